@@ -1,0 +1,227 @@
+/* tt_hip.h — C ABI of libtt_hip.so, the MI355X (gfx950) implementation of the
+ * two-tower contrastive training step of mateomarin/two_towers.
+ *
+ * The reference has no native code and no FFI: its hot path is PyTorch module calls
+ * (nn.GRU, nn.Linear, nn.LayerNorm, F.normalize, matmul, cross_entropy,
+ * cosine_similarity, topk, optim.Adam). Each entry point below replaces one of those
+ * call sites; the reference file:line it stands in for is given per function.
+ * two_towers_amd/ (Python, ctypes) binds these entry points behind the reference's
+ * own nn.Module surface (EnhancedTwoTowerModel, InfoNCELoss, MarginRankingLoss,
+ * get_hard_negatives).
+ *
+ * Conventions
+ *  - All pointers are device pointers (HBM) owned by the caller; nothing here
+ *    allocates device memory. Scratch ("ws") is caller-provided.
+ *  - dtype selects storage/arithmetic of the tensor operands: TT_DT_F32 (exact fp32
+ *    MFMA) or TT_DT_BF16 (bf16 storage, fp32 accumulation). Tensors typed `float*`
+ *    are always fp32.
+ *  - Matrices are row-major with an explicit leading dimension in ELEMENTS.
+ *  - stream is a hipStream_t (NULL = default stream); every call is stream-ordered
+ *    and asynchronous. Thread-safe on distinct streams.
+ *  - Return 0 on success, TT_EINVAL on a bad argument, else a hipError_t code;
+ *    tt_last_error() returns a thread-local message for the last failure.
+ */
+#ifndef TT_HIP_H
+#define TT_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TT_OK 0
+#define TT_EINVAL 1000
+#define TT_DT_F32 0
+#define TT_DT_BF16 1
+
+/* Library version string, e.g. "tt_hip 0.1.0 gfx950". */
+const char* tt_version(void);
+/* Message describing the last non-zero return on this thread ("" if none). */
+const char* tt_last_error(void);
+
+/* ---------------------------------------------------------------- featurisation */
+/* Word2Vec row gather: out[i, :] = table[ids[i], :] for ids[i] >= 0, zero row for
+ * ids[i] < 0 (pad / all-OOV).  Replaces the per-word lookup + zero padding of
+ * EnhancedDataset.text_to_embedding (enhanced_two_tower.py:144-166).
+ * table [vocab, ep], out [n, ep]; ep * sizeof(dtype) must be a multiple of 16. */
+int tt_embed_gather(int dtype, const void* table, long vocab, int ep, const int32_t* ids, long n,
+                    void* out, void* stream);
+
+/* Packs float rows [n, e] into dtype rows [n, ep] (zero columns e..ep-1): the
+ * reference's float [B,T,E] encoder input (enhanced_two_tower.py:50,56) into the
+ * padded layout the projections read. */
+int tt_pack_rows(int dtype, const float* src, long n, int e, int ep, void* out, void* stream);
+
+/* y[i] = (dtype)x[i] (fp32 -> dtype) for n elements. */
+int tt_cast(int dtype, const float* x, long n, void* y, void* stream);
+
+/* out[c] (+)= sum_r x[r*ld + c] over r < rows (x fp32). Bias gradients. */
+int tt_colsum(const float* x, long rows, int cols, long ld, float* out, int accumulate, void* stream);
+
+/* ------------------------------------------------------------------------ GEMM */
+/* Batched MFMA GEMM (up to 4 independent problems of one shape per launch):
+ *     C_b[m][n] = alpha * sum_k A_b(m,k) B_b(n,k) (+ bias_b[n]) (relu) (*dropmask) (+ C_b)
+ * a_kouter = 0: A stored [m][k] (lda);   1: A stored [k][m] (lda).
+ * b_kouter = 0: B stored [n][k] (ldb);   1: B stored [k][n] (ldb).
+ * With b_kouter = 1 and bshift[b] != 0, B row k is read from row k + shift when
+ * (k mod seq_t) + shift lies in [0, seq_t), else treated as zero (GRU h_{t-1} operand).
+ * drop_p > 0 multiplies element (m, n) by the counter-based dropout mask
+ * keep(drop_seed, m, n) / (1 - drop_p) (see tt_gru_fwd).
+ * splits > 1 splits K across workgroups: fp32 partials go to splitk_ws
+ * (tt_gemm_ws_size floats) and are reduced into C; relu/dropout unsupported then.
+ * out_dtype is TT_DT_F32 or dtype. Any m, n, k; operand base pointers and leading
+ * dimensions must be 16-byte aligned (lda * sizeof(dtype) % 16 == 0). */
+typedef struct {
+  const void* a[4];
+  const void* b[4];
+  void* c[4];
+  const float* bias[4];
+  int bshift[4];
+} tt_gemm_batch;
+
+int tt_gemm(int dtype, int out_dtype, int a_kouter, int b_kouter, int m, int n, int k,
+            const tt_gemm_batch* batch, int nbatch, long lda, long ldb, long ldc, float alpha,
+            int beta_accum, int relu, int seq_t, uint32_t drop_seed, float drop_p, int splits,
+            float* splitk_ws, void* stream);
+long tt_gemm_ws_size(int m, int n, int nbatch, int splits);
+/* Heuristic split count for a (m, n, k, nbatch) problem. */
+int tt_gemm_pick_splits(int m, int n, int k, int nbatch);
+
+/* ------------------------------------------------------------------------- GRU */
+/* One bidirectional GRU layer, forward, all time steps (torch nn.GRU semantics:
+ * r = s(Wir x + bir + Whr h + bhr), z = s(Wiz x + biz + Whz h + bhz),
+ * n = tanh(Win x + bin + r*(Whn h + bhn)), h' = (1-z) n + z h, h0 = 0).
+ * Replaces nn.GRU at enhanced_two_tower.py:51,57 (per layer, up to 4 recurrences =
+ * {query,doc} x {fwd,rev} per launch). The input projection g = x Wih^T + bih
+ * (+ [bhr, bhz, 0]) is a tt_gemm done by the caller. */
+typedef struct {
+  const void* g;       /* [B*T, ldg]: gate pre-activations r|z|n (3H columns)        */
+  const void* whh;     /* [3H, H]                                                    */
+  const float* bhn;    /* [H]                                                        */
+  void* y;             /* h_t: element (b,t,j) at y[(b*T+t)*ldy + j]                 */
+  void* x1;            /* optional dropout(y) for the next layer (same layout) or NULL */
+  void* save;          /* [B*T, 4H] saved pre-activations of r|z|n and gh_n (backward) */
+  float* hstate;       /* fp32 scratch [2][B][H]                                     */
+  int dir;             /* 0: t = 0..T-1 ; 1: t = T-1..0                              */
+  uint32_t drop_seed;  /* dropout stream of x1                                       */
+  int drop_col0;       /* column of this recurrence inside the layer output (dir*H)  */
+} tt_gru_fwd_rec;
+
+int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B, int T, int H, long ldg,
+               long ldy, float drop_p, void* stream);
+
+/* Backward (BPTT) of tt_gru_fwd. Produces dL/dg (= dgx, feeds dWih, dbih and the
+ * layer-input gradient) and dL/dgh (feeds dWhh), plus per-tile bias partial sums
+ * (columns r|z|n|ghn, reduce with tt_colsum: dbih = [0:3H], dbhh = [0:2H],[3H:4H]). */
+typedef struct {
+  const void* save;    /* [B*T, 4H] from tt_gru_fwd          */
+  const void* y;       /* layer output (source of h_{s-1})   */
+  const void* dy;      /* dL/dy (ldy) or NULL                */
+  const float* dfinal; /* dL/dh_final [B, ldf] or NULL       */
+  const void* whh;     /* [3H, H]                            */
+  void* dgx;           /* [B*T, ldd]                         */
+  void* dgh;           /* [B*T, ldd]                         */
+  float* dhstate;      /* fp32 scratch [2][B][H]             */
+  float* dbias_part;   /* fp32 [tt_gru_bias_rows(B)][4H]; zeroed by tt_gru_bwd */
+  int dir;
+} tt_gru_bwd_rec;
+
+int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B, int T, int H, long ldy,
+               long ldd, long ldf, void* stream);
+int tt_gru_bias_rows(int B);
+
+/* ------------------------------------------------------------ projection head */
+/* Linear(4h->2h) -> LayerNorm(2h, eps) -> ReLU -> Linear(2h->h), fwd and bwd.
+ * Replaces query_proj/doc_proj (enhanced_two_tower.py:36-48, applied :54,60).
+ * Weights in dtype (w1 [2h,4h], w2 [h,2h]); biases/LN affine fp32. */
+typedef struct {
+  const void* w1; const float* b1; const float* ln_g; const float* ln_b;
+  const void* w2; const float* b2;
+  const void* x;   /* [B, 4h] dtype : cat(h_fwd_final, h_rev_final)            */
+  void* p1;        /* [B, 2h] dtype : saved pre-LayerNorm activations           */
+  float* mean;     /* [B]                                                       */
+  float* rstd;     /* [B]                                                       */
+  void* u;         /* [B, 2h] dtype : saved post-ReLU activations               */
+  float* out;      /* [B, h]  fp32                                              */
+} tt_head_fwd_io;
+
+int tt_proj_head_fwd(int dtype, const tt_head_fwd_io* io, int ntower, int B, int h, float ln_eps,
+                     void* stream);
+
+typedef struct {
+  const void* w1; const float* ln_g; const float* ln_b; const void* w2;
+  const void* x; const void* p1; const float* mean; const float* rstd; const void* u;
+  const float* dout;  /* [B, h] fp32 upstream gradient                              */
+  float* dx;          /* [B, 4h] fp32 gradient wrt x                                */
+  float* dw1; float* db1; float* dg; float* dbeta; float* dw2; float* db2;  /* fp32 grads (overwritten) */
+  void* ws;           /* scratch, tt_proj_head_bwd_ws_size bytes                     */
+} tt_head_bwd_io;
+
+int tt_proj_head_bwd(int dtype, const tt_head_bwd_io* io, int ntower, int B, int h, float ln_eps,
+                     void* stream);
+long tt_proj_head_bwd_ws_size(int dtype, int B, int h);
+
+/* ---------------------------------------------------------------------- losses */
+/* y = x / max(||x||_2, eps) row-wise (F.normalize, enhanced_two_tower.py:74-75; also
+ * the normalisation inside F.cosine_similarity, :112-117,125-128). y in dtype, y32
+ * optional fp32 copy, norm[rows] fp32 = ||x||. */
+int tt_l2norm_fwd(int dtype, const float* x, long rows, int cols, float eps, void* y, float* y32,
+                  float* norm, void* stream);
+/* dx (+)= (dy - y (y.dy)) / max(||x||, eps)  (dy, y32 fp32). */
+int tt_l2norm_bwd(const float* dy, const float* y32, const float* norm, long rows, int cols,
+                  float eps, float* dx, int accumulate, void* stream);
+
+/* InfoNCE / in-batch softmax cross-entropy over S = inv_tau * qn dn^T
+ * (enhanced_two_tower.py:78-82). offdiag_sub is subtracted from every S_ij with
+ * j != label_i: the in-batch branch of MarginRankingLoss (:92-101) uses
+ * offdiag_sub = margin on un-normalised inputs.
+ * Row i's label column is label_offset + i. The B x N score matrix is never written:
+ * each workgroup streams dn tiles through one fused MFMA kernel with a running
+ * log-sum-exp. Outputs lse[i] and row_loss[i] = lse[i] - S[i][label]. */
+int tt_infonce_fwd(int dtype, const void* qn, long bq, const void* dn, long nd, int h,
+                   float inv_tau, float offdiag_sub, long label_offset, float* lse,
+                   float* row_loss, void* ws, void* stream);
+long tt_infonce_fwd_ws_size(long bq, long nd);
+/* Gradient of gscale * sum_i row_loss[i]: dqn [bq,h], ddn [nd,h] (fp32, overwritten).
+ * ws: tt_infonce_bwd_ws_size bytes. */
+int tt_infonce_bwd(int dtype, const void* qn, long bq, const void* dn, long nd, int h,
+                   float inv_tau, float offdiag_sub, long label_offset, const float* lse,
+                   float gscale, float* dqn, float* ddn, void* ws, void* stream);
+long tt_infonce_bwd_ws_size(int dtype, long bq, long nd, int h);
+
+/* Hard-negative mining, batched over rows (get_hard_negatives,
+ * enhanced_two_tower.py:123-133): sims = qn dn^T (cosine for normalised inputs), the
+ * positive column label_offset+i set to -1 (label_offset < 0: no column masked), top-k (k <= 8) indices per row sorted by
+ * descending similarity; ties broken towards the lower column index.
+ * idx [bq, k] int32, val [bq, k] fp32 (optional). ws: tt_hardneg_ws_size bytes. */
+int tt_hardneg_topk(int dtype, const void* qn, long bq, const void* dn, long nd, int h,
+                    long label_offset, int k, int32_t* idx, float* val, void* ws, void* stream);
+long tt_hardneg_ws_size(int dtype, long bq, long nd);
+
+/* MarginRankingLoss with explicit negatives (enhanced_two_tower.py:102-121) on
+ * normalised vectors: pos_i = qn_i.dn_{label_offset+i}, negm_i = mean_j qn_i.dn_{idx[i,j]},
+ * row_loss_i = max(margin - pos_i + negm_i, 0). Negatives are rows of dn. */
+int tt_margin_fwd(const float* qn, long bq, const float* dn, long nd, int h, long label_offset,
+                  const int32_t* idx, int k, float margin, float* row_loss, void* stream);
+/* Gradient of gscale * sum_i row_loss_i: dqn (overwritten), ddn (accumulated; the
+ * caller zeroes it). */
+int tt_margin_bwd(const float* qn, long bq, const float* dn, long nd, int h, long label_offset,
+                  const int32_t* idx, int k, float margin, float gscale, float* dqn, float* ddn,
+                  void* stream);
+
+/* out[0] = scale * sum_i x[i]. */
+int tt_sum(const float* x, long n, float scale, float* out, void* stream);
+
+/* ------------------------------------------------------------------- optimiser */
+/* torch.optim.Adam (train_enhanced.py:43,63) over up to 48 fp32 tensors per call,
+ * bit-for-bit the update order of torch's single-tensor Adam:
+ *   m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2 ;
+ *   p -= lr/(1-b1^step) * m / (sqrt(v)/sqrt(1-b2^step) + eps)   (g += wd*p first). */
+int tt_adam_multi(float* const* params, const float* const* grads, float* const* exp_avg,
+                  float* const* exp_avg_sq, const long* sizes, int ntensors, float lr, float beta1,
+                  float beta2, float eps, float weight_decay, int step, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TT_HIP_H */

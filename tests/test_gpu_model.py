@@ -1,0 +1,138 @@
+"""Model-level parity on the GPU against the CPU oracle (oracle/cpu_ref.py)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import two_towers_amd as tta  # noqa: E402
+from oracle import cpu_ref  # noqa: E402
+
+DEV = "cuda"
+
+
+def make_model(E, h, seed=0):
+    torch.manual_seed(seed)
+    m = tta.EnhancedTwoTowerModel(E, h)
+    p = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    return m, p
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-12))
+
+
+@pytest.mark.parametrize("E,h,B,T", [(16, 8, 16, 8), (40, 32, 100, 12), (300, 64, 64, 16)])
+def test_forward_backward_fp32(E, h, B, T):
+    m, p = make_model(E, h)
+    m = m.to(DEV).eval()
+    g = torch.Generator().manual_seed(5)
+    q = torch.randn(B, T, E, generator=g)
+    d = torch.randn(B, T, E, generator=g)
+    qv, dv = m(q.to(DEV), d.to(DEV))
+    loss = tta.InfoNCELoss()(qv, dv)
+    loss.backward()
+    pr = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    rq, rd = cpu_ref.forward(q, d, pr)
+    rl = cpu_ref.infonce(rq, rd)
+    rl.backward()
+    assert rel(qv, rq) < 1e-4 and rel(dv, rd) < 1e-4
+    assert abs(float(loss) - float(rl)) < 1e-4 * max(1.0, abs(float(rl)))
+    named = dict(m.named_parameters())
+    worst = max(rel(named[k].grad, pr[k].grad) for k in pr)
+    assert worst < 2e-3, {k: rel(named[k].grad, pr[k].grad) for k in pr}
+
+
+def test_forward_backward_bf16():
+    E, h, B, T = 64, 32, 96, 10
+    m, p = make_model(E, h, 1)
+    m = m.to(DEV).eval().set_compute_dtype(torch.bfloat16)
+    g = torch.Generator().manual_seed(6)
+    q = torch.randn(B, T, E, generator=g)
+    d = torch.randn(B, T, E, generator=g)
+    qv, dv = m(q.to(DEV), d.to(DEV))
+    loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
+    loss.backward()
+    pr = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    rq, rd = cpu_ref.forward(q, d, pr)
+    rl = cpu_ref.infonce(rq, rd)
+    rl.backward()
+    assert rel(qv, rq) < 3e-2 and rel(dv, rd) < 3e-2
+    assert abs(float(loss) - float(rl)) < 2e-2 * abs(float(rl))
+    named = dict(m.named_parameters())
+    errs = {k: rel(named[k].grad, pr[k].grad) for k in pr}
+    assert max(errs.values()) < 5e-2, errs
+
+
+def test_dropout_matches_counter_mask():
+    E, h, B, T = 24, 16, 40, 6
+    m, p = make_model(E, h, 2)
+    m = m.to(DEV).train()
+    g = torch.Generator().manual_seed(7)
+    q = torch.randn(B, T, E, generator=g)
+    torch.manual_seed(99)
+    qv = m.encode_query(q.to(DEV))
+    torch.manual_seed(99)
+    seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+    rq = cpu_ref.encode(q, p, "query", drop_p=0.1, seed=seed)
+    assert rel(qv, rq) < 1e-4
+
+
+def test_margin_hardneg_fp32():
+    B, h = 64, 16
+    g = torch.Generator().manual_seed(8)
+    q = torch.randn(B, h, generator=g)
+    d = torch.randn(B, h, generator=g)
+    qd, dd = q.clone().to(DEV).requires_grad_(True), d.clone().to(DEV).requires_grad_(True)
+    lossf = tta.HardNegativeMarginLoss(k=5, margin=0.2)
+    loss = lossf(qd, dd)
+    loss.backward()
+    qr, dr = q.clone().requires_grad_(True), d.clone().requires_grad_(True)
+    rl, ridx = cpu_ref.hardneg_margin(qr, dr, 5, 0.2)
+    rl.backward()
+    assert torch.equal(lossf.last_indices.long().cpu(), ridx)
+    assert abs(float(loss) - float(rl)) < 1e-5
+    assert rel(qd.grad, qr.grad) < 1e-4 and rel(dd.grad, dr.grad) < 1e-4
+
+
+def test_margin_inbatch_and_explicit():
+    B, h, k = 32, 24, 3
+    g = torch.Generator().manual_seed(9)
+    q, d, n = torch.randn(B, h, generator=g), torch.randn(B, h, generator=g), torch.randn(B * k, h, generator=g)
+    for neg in (None, n):
+        ts = [t.clone().to(DEV).requires_grad_(True) for t in (q, d)] + ([n.clone().to(DEV).requires_grad_(True)] if neg is not None else [])
+        rs = [t.clone().requires_grad_(True) for t in (q, d)] + ([n.clone().requires_grad_(True)] if neg is not None else [])
+        l1 = tta.MarginRankingLoss()(*ts)
+        l2 = cpu_ref.margin_loss(*rs)
+        l1.backward()
+        l2.backward()
+        assert abs(float(l1) - float(l2)) < 1e-4 * max(1, abs(float(l2)))
+        for a, b in zip(ts, rs):
+            assert rel(a.grad, b.grad) < 1e-4
+
+
+def test_get_hard_negatives_single():
+    g = torch.Generator().manual_seed(10)
+    q = torch.randn(32, generator=g)
+    docs = torch.randn(500, 32, generator=g)
+    idx = tta.get_hard_negatives(q.to(DEV), docs.to(DEV), 17, k=5)
+    assert torch.equal(idx.cpu(), cpu_ref.hard_negatives(q, docs, 17, 5))
+
+
+def test_token_ids_match_float_inputs():
+    E, h, B, T, V = 32, 16, 20, 9, 50
+    m, p = make_model(E, h, 3)
+    m = m.to(DEV).eval()
+    table = torch.randn(V, E)
+    ids = torch.randint(-1, V, (B, T), dtype=torch.int32)
+    emb = torch.where((ids >= 0)[..., None], table[ids.clamp_min(0).long()], torch.zeros(E))
+    m.set_embedding_table(table.to(DEV))
+    a = m.encode_doc(ids.to(DEV))
+    b = m.encode_doc(emb.to(DEV))
+    assert torch.allclose(a, b, rtol=0, atol=0)
+
+
+def test_cpu_tensors_fail_loudly():
+    m, _ = make_model(16, 8)
+    with pytest.raises(RuntimeError, match="GPU"):
+        m(torch.randn(2, 3, 16), torch.randn(2, 3, 16))

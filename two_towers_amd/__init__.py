@@ -1,0 +1,19 @@
+"""two_towers_amd — MI355X-native two-tower contrastive training step.
+
+Drop-in for the hot path of mateomarin/two_towers (train_enhanced.py:54-69): the
+EnhancedTwoTowerModel / InfoNCELoss / MarginRankingLoss / get_hard_negatives surface
+of enhanced_two_tower.py, computed by hand-written HIP kernels for gfx950
+(libtt_hip.so, C ABI in include/tt_hip.h). There is no CPU fallback.
+"""
+from .data import (EnhancedDataset, EnhancedIdDataset, MSMarcoDataset, Vocab, encode_batch, encode_ids,
+                   load_ms_marco_train, load_word2vec, pairs_from_msmarco)
+from .losses import HardNegativeMarginLoss, InfoNCELoss, MarginRankingLoss, get_hard_negatives, mine_hard_negatives
+from .model import EnhancedTwoTower, EnhancedTwoTowerModel
+from .optim import Adam
+
+__all__ = [
+    "EnhancedTwoTowerModel", "EnhancedTwoTower", "InfoNCELoss", "MarginRankingLoss", "HardNegativeMarginLoss",
+    "get_hard_negatives", "mine_hard_negatives", "EnhancedDataset", "EnhancedIdDataset", "MSMarcoDataset",
+    "Vocab", "encode_ids", "encode_batch", "load_word2vec", "load_ms_marco_train", "pairs_from_msmarco", "Adam",
+]
+__version__ = "0.1.0"

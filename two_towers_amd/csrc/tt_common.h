@@ -1,0 +1,86 @@
+// Shared device helpers for the two-tower HIP path (gfx950 / CDNA4 only).
+//
+// Element types: the path runs in one of two arithmetic types, chosen per call:
+//   TT_F32  = 0 : fp32 storage, exact-f32 MFMA (v_mfma_f32_16x16x4_f32)
+//   TT_BF16 = 1 : bf16 storage, v_mfma_f32_16x16x32_bf16, fp32 accumulation
+// bf16 values travel as raw uint16_t bits so no HIP bf16 class is needed.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define TT_F32 0
+#define TT_BF16 1
+
+typedef uint16_t bf16_t;
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define TT_DEV __device__ __forceinline__
+
+TT_DEV float bf2f(bf16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
+// Round-to-nearest-even; lowers to v_cvt_pk_bf16_f32 (keeps NaN a NaN).
+TT_DEV bf16_t f2bf(float f) { __bf16 h = (__bf16)f; return __builtin_bit_cast(bf16_t, h); }
+
+template <typename T> struct Elt;
+template <> struct Elt<float> {
+  static constexpr int EPC = 4;  // elements per 16-byte chunk
+  TT_DEV static float ld(const float* p) { return *p; }
+  TT_DEV static void st(float* p, float v) { *p = v; }
+  TT_DEV static float cvt(float v) { return v; }
+};
+template <> struct Elt<bf16_t> {
+  static constexpr int EPC = 8;
+  TT_DEV static float ld(const bf16_t* p) { return bf2f(*p); }
+  TT_DEV static void st(bf16_t* p, float v) { *p = f2bf(v); }
+  TT_DEV static bf16_t cvt(float v) { return f2bf(v); }
+};
+
+TT_DEV float tt_sigmoid(float x) { return 1.0f / (1.0f + __expf(-x)); }
+TT_DEV float tt_tanh(float x) {
+  // tanh(x) = 1 - 2/(exp(2x)+1); saturates cleanly for large |x|.
+  float e = __expf(2.0f * x);
+  return 1.0f - 2.0f / (e + 1.0f);
+}
+
+// 1 - tanh(x)^2 without cancellation: 4 e^{-2|x|} / (1 + e^{-2|x|})^2.
+TT_DEV float tt_sech2(float x) {
+  const float e = __expf(-2.0f * fabsf(x));
+  const float d = 1.0f + e;
+  return 4.0f * e / (d * d);
+}
+
+// Counter-based dropout mask shared by the forward (GRU layer-0 output) and
+// backward (input-projection gradient) kernels, and restated in oracle/.
+// keep(seed, row, col) with row = b*T + t, col in [0, 2H).
+TT_DEV uint32_t tt_hash3(uint32_t seed, uint32_t row, uint32_t col) {
+  uint32_t h = seed * 0x9E3779B1u ^ (row * 0x85EBCA77u) ^ (col * 0xC2B2AE3Du + 0x27D4EB2Fu);
+  h ^= h >> 16; h *= 0x7FEB352Du; h ^= h >> 15; h *= 0x846CA68Bu; h ^= h >> 16;
+  return h;
+}
+// Returns the multiplier (0 or 1/(1-p)); threshold = p * 2^24.
+TT_DEV float tt_dropout_scale(uint32_t seed, uint32_t row, uint32_t col, uint32_t thresh, float inv_keep) {
+  return ((tt_hash3(seed, row, col) >> 8) < thresh) ? 0.0f : inv_keep;
+}
+
+TT_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+TT_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// Reduce over the 16 lanes that share (lane>>4) — one MFMA C-tile row group.
+TT_DEV float sum16(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+TT_DEV float max16(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}

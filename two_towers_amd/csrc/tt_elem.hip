@@ -1,0 +1,126 @@
+// HBM-bound helpers: Word2Vec row gather, float->padded packing, casts, column sums.
+#include <algorithm>
+
+#include "tt_api.h"
+#include "tt_common.h"
+
+namespace {
+
+// One 16-byte chunk per thread; consecutive threads walk a row, so both the
+// table row read and the output row write are fully coalesced 16 B/lane.
+__global__ __launch_bounds__(256) void embed_gather_kernel(const uint4* __restrict__ table, long vocab,
+                                                           int cpr, const int32_t* __restrict__ ids,
+                                                           long n, uint4* __restrict__ out) {
+  const long total = n * cpr;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const long row = e / cpr;
+    const int c = (int)(e - row * cpr);
+    const int id = ids[row];
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (id >= 0 && id < vocab) v = table[(long)id * cpr + c];
+    out[e] = v;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void pack_rows_kernel(const float* __restrict__ src, long n, int e, int ep,
+                                                        T* __restrict__ out) {
+  const long total = n * ep;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long r = i / ep;
+    const int c = (int)(i - r * ep);
+    Elt<T>::st(out + i, c < e ? src[r * e + c] : 0.f);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void cast_kernel(const float* __restrict__ x, long n, T* __restrict__ y) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) Elt<T>::st(y + i, x[i]);
+}
+
+// Column sums: grid.x over column blocks of 256, grid.y over row slabs; one fp32
+// atomic per (slab, column).
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ x, long rows, int cols, long ld,
+                                                     long rows_per_slab, float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  const long r0 = (long)blockIdx.y * rows_per_slab;
+  const long r1 = std::min(rows, r0 + rows_per_slab);
+  float s = 0.f;
+  for (long r = r0; r < r1; ++r) s += x[r * ld + c];
+  atomicAdd(out + c, s);
+}
+
+__global__ __launch_bounds__(256) void sum_kernel(const float* __restrict__ x, long n, float scale,
+                                                  float* __restrict__ out) {
+  __shared__ float part[4];
+  float s = 0.f;
+  for (long i = threadIdx.x; i < n; i += 256) s += x[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = scale * (part[0] + part[1] + part[2] + part[3]);
+}
+
+inline unsigned grid_for(long work, int per_block = 256, int cap = 8192) {
+  long g = (work + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  return (unsigned)std::min<long>(g, cap);
+}
+
+}  // namespace
+
+extern "C" int tt_embed_gather(int dtype, const void* table, long vocab, int ep, const int32_t* ids, long n,
+                               void* out, void* stream) {
+  TT_CHECK_ARG(dtype == TT_DT_F32 || dtype == TT_DT_BF16, "tt_embed_gather: bad dtype");
+  const int esz = dtype == TT_DT_BF16 ? 2 : 4;
+  TT_CHECK_ARG((ep * esz) % 16 == 0, "tt_embed_gather: ep*sizeof(dtype) must be a multiple of 16 (ep=%d)", ep);
+  if (n == 0) return 0;
+  const int cpr = ep * esz / 16;
+  hipLaunchKernelGGL(embed_gather_kernel, dim3(grid_for(n * cpr)), dim3(256), 0, (hipStream_t)stream,
+                     (const uint4*)table, vocab, cpr, ids, n, (uint4*)out);
+  TT_CHECK_LAUNCH("embed_gather_kernel");
+  return 0;
+}
+
+extern "C" int tt_pack_rows(int dtype, const float* src, long n, int e, int ep, void* out, void* stream) {
+  TT_CHECK_ARG(ep >= e, "tt_pack_rows: ep < e");
+  if (n == 0) return 0;
+  dim3 g(grid_for(n * ep));
+  if (dtype == TT_DT_BF16)
+    hipLaunchKernelGGL(pack_rows_kernel<bf16_t>, g, dim3(256), 0, (hipStream_t)stream, src, n, e, ep, (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(pack_rows_kernel<float>, g, dim3(256), 0, (hipStream_t)stream, src, n, e, ep, (float*)out);
+  TT_CHECK_LAUNCH("pack_rows_kernel");
+  return 0;
+}
+
+extern "C" int tt_cast(int dtype, const float* x, long n, void* y, void* stream) {
+  if (n == 0) return 0;
+  dim3 g(grid_for(n));
+  if (dtype == TT_DT_BF16)
+    hipLaunchKernelGGL(cast_kernel<bf16_t>, g, dim3(256), 0, (hipStream_t)stream, x, n, (bf16_t*)y);
+  else
+    hipLaunchKernelGGL(cast_kernel<float>, g, dim3(256), 0, (hipStream_t)stream, x, n, (float*)y);
+  TT_CHECK_LAUNCH("cast_kernel");
+  return 0;
+}
+
+extern "C" int tt_colsum(const float* x, long rows, int cols, long ld, float* out, int accumulate, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!accumulate) TT_CHECK_HIP(hipMemsetAsync(out, 0, sizeof(float) * cols, st));
+  if (rows == 0 || cols == 0) return 0;
+  const int cb = tt_ceil_div(cols, 256);
+  long slabs = std::max<long>(1, std::min<long>(rows / 64, 2048 / cb));
+  const long rps = (rows + slabs - 1) / slabs;
+  slabs = (rows + rps - 1) / rps;
+  hipLaunchKernelGGL(colsum_kernel, dim3(cb, (unsigned)slabs), dim3(256), 0, st, x, rows, cols, ld, rps, out);
+  TT_CHECK_LAUNCH("colsum_kernel");
+  return 0;
+}
+
+extern "C" int tt_sum(const float* x, long n, float scale, float* out, void* stream) {
+  hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, x, n, scale, out);
+  TT_CHECK_LAUNCH("sum_kernel");
+  return 0;
+}

@@ -1,0 +1,257 @@
+// MFMA GEMM main loop shared by every contraction on the path (input projections,
+// GRU step GEMMs, weight gradients, projection head).
+//
+// One 256-thread workgroup (4 waves as 2x2) computes a BM x BN fp32 tile of
+//     C[m][n] = sum_k A(m,k) * B(n,k)
+// Each operand is staged through LDS in one of two layouts:
+//   K-contig ("KC"): element (r,k) at row r, k contiguous   -> LDS image [rows][128 B]
+//   K-outer  ("KO"): element (r,k) at row k, r contiguous   -> LDS image [k][rows]
+// so NT, NN and TN products all run on the same loop (no transposed copies).
+//
+// A K-tile is 128 bytes of K per row (64 bf16 or 32 fp32); it is consumed in two
+// 64-byte sub-steps. One 16-byte LDS chunk of a KC row holds 8 bf16 / 4 fp32 k-values:
+//   bf16: lane l reads 16 B at chunk (l>>4)+4*ks -> k = 8*(l>>4)+j, exactly the
+//         v_mfma_f32_16x16x32_bf16 fragment.
+//   fp32: the same 16 B are 4 k-values; four v_mfma_f32_16x16x4_f32 consume them
+//         with k permuted identically on A and B, so the sum is unchanged.
+// KO images are read with ds_read_b64_tr_b16 (bf16) or ds_read_b32 (fp32).
+// All images are XOR-swizzled so that the fragment reads are bank-conflict free
+// (verified against the gfx950 lane groups in tools/check_swizzle.py).
+#pragma once
+#include "tt_common.h"
+
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+namespace ttg {
+
+constexpr int KTB = 128;  // K-tile bytes per row
+
+// ---- LDS byte offsets --------------------------------------------------------
+// KC image: rows of 128 B, 16-B chunk c stored at c ^ ((row>>1)&7).
+TT_DEV int kc_off(int row, int c) { return row * KTB + ((c ^ ((row >> 1) & 7)) << 4); }
+// KO bf16 image: k-rows of 256 B (128 columns), 16-B chunk c stored at c ^ 2v(k).
+TT_DEV int ko_v(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+TT_DEV int ko16_off(int k, int c) { return k * 256 + ((c ^ (ko_v(k) << 1)) << 4); }
+// KO fp32 image: k-rows of 512 B (128 columns), column m stored at m ^ 16*((k>>2)&1).
+TT_DEV int ko32_off_chunk(int k, int c) { return k * 512 + ((c ^ (((k >> 2) & 1) << 2)) << 4); }
+TT_DEV int ko32_off_elem(int k, int m) { return k * 512 + ((m ^ (((k >> 2) & 1) << 4)) << 2); }
+
+template <typename T, bool KO, int ROWS>
+struct Img {
+  // bytes of one stage of this operand's image
+  static constexpr int BYTES = KO ? (KTB / (int)sizeof(T)) * ROWS * (int)sizeof(T) : ROWS * KTB;
+  static constexpr int CHUNKS = BYTES / 16;
+  static_assert(!KO || ROWS == 128, "K-outer images are 128 columns wide");
+};
+
+// ---- loaders -------------------------------------------------------------------
+// A KC loader provides rowptr(r): pointer to element (r, k=0) of tile-row r, or nullptr.
+// A KO loader provides kptr(k): pointer to element (k, tile column 0), or nullptr,
+// and ncols: number of valid tile columns (tail).
+
+// First n (< elements per chunk) elements of a 16-byte chunk, zero-filled: the
+// K (or column) tail of an operand whose extent is not a multiple of 16 bytes.
+template <typename T>
+TT_DEV uint4 load_partial(const T* p, int n) {
+  union {
+    uint4 v;
+    T e[16 / sizeof(T)];
+  } u;
+  u.v = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int i = 0; i < (int)(16 / sizeof(T)); ++i)
+    if (i < n) u.e[i] = p[i];
+  return u.v;
+}
+
+template <typename T, bool KO, int ROWS, class L>
+TT_DEV void stage_load(const L& ld, int kt, int K, uint4 (&r)[Img<T, KO, ROWS>::CHUNKS / 256]) {
+  constexpr int N = Img<T, KO, ROWS>::CHUNKS / 256;
+  constexpr int EPC = Elt<T>::EPC;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int id = tid + 256 * i;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if constexpr (!KO) {
+      const int row = id >> 3, c = id & 7;
+      const T* p = ld.rowptr(row);
+      const int k = kt * (KTB / (int)sizeof(T)) + c * EPC;
+      if (p != nullptr && k < K) v = (k + EPC <= K) ? *reinterpret_cast<const uint4*>(p + k) : load_partial(p + k, K - k);
+    } else {
+      constexpr int CPR = ROWS * (int)sizeof(T) / 16;  // chunks per k-row
+      const int kl = id / CPR, c = id % CPR;
+      const int k = kt * (KTB / (int)sizeof(T)) + kl;
+      const T* p = (k < K) ? ld.kptr(k) : nullptr;
+      const int col = c * EPC;
+      if (p != nullptr && col < ld.ncols)
+        v = (col + EPC <= ld.ncols) ? *reinterpret_cast<const uint4*>(p + col) : load_partial(p + col, ld.ncols - col);
+    }
+    r[i] = v;
+  }
+}
+
+template <typename T, bool KO, int ROWS>
+TT_DEV void stage_store(char* img, const uint4 (&r)[Img<T, KO, ROWS>::CHUNKS / 256]) {
+  constexpr int N = Img<T, KO, ROWS>::CHUNKS / 256;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int id = tid + 256 * i;
+    int off;
+    if constexpr (!KO) {
+      off = kc_off(id >> 3, id & 7);
+    } else if constexpr (sizeof(T) == 2) {
+      off = ko16_off(id >> 4, id & 15);
+    } else {
+      off = ko32_off_chunk(id >> 5, id & 31);
+    }
+    *reinterpret_cast<uint4*>(img + off) = r[i];
+  }
+}
+
+// Fragment of a 16-row (or 16-column) slab starting at tile row r0, sub-step ks.
+// Returned as 16 bytes: bf16x8 for bf16, f32x4 for fp32.
+template <typename T, bool KO>
+TT_DEV uint4 frag(const char* img, int r0, int ks) {
+  const int lane = threadIdx.x & 63;
+  if constexpr (!KO) {
+    const int row = r0 + (lane & 15);
+    const int c = (lane >> 4) + 4 * ks;
+    return *reinterpret_cast<const uint4*>(img + kc_off(row, c));
+  } else if constexpr (sizeof(T) == 2) {
+    const int g = lane >> 4, i4 = lane & 15, q = i4 >> 2, p = i4 & 3;
+    const int k0 = ks * 32 + 8 * g + q;
+    const int cc = (r0 >> 2) + p;  // 8-byte chunk along the row
+    const int k1 = k0 + 4;
+    const int o0 = ko16_off(k0, cc >> 1) + ((cc & 1) << 3);
+    const int o1 = ko16_off(k1, cc >> 1) + ((cc & 1) << 3);
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + o0));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + o1));
+    uint4 v;
+    v.x = (uint32_t)(uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16);
+    v.y = (uint32_t)(uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16);
+    v.z = (uint32_t)(uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16);
+    v.w = (uint32_t)(uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16);
+    return v;
+  } else {
+    const int g = lane >> 4;
+    const int m = r0 + (lane & 15);
+    const int kb = ks * 16 + 4 * g;
+    uint4 v;
+    v.x = *reinterpret_cast<const uint32_t*>(img + ko32_off_elem(kb + 0, m));
+    v.y = *reinterpret_cast<const uint32_t*>(img + ko32_off_elem(kb + 1, m));
+    v.z = *reinterpret_cast<const uint32_t*>(img + ko32_off_elem(kb + 2, m));
+    v.w = *reinterpret_cast<const uint32_t*>(img + ko32_off_elem(kb + 3, m));
+    return v;
+  }
+}
+
+template <typename T>
+TT_DEV f32x4 mma(uint4 a, uint4 b, f32x4 c) {
+  if constexpr (sizeof(T) == 2) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8v, a),
+                                                   __builtin_bit_cast(bf16x8v, b), c, 0, 0, 0);
+  } else {
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), c, 0, 0, 0);
+    return c;
+  }
+}
+
+template <typename T, bool AKO, bool BKO, int BM, int BN>
+struct MainLoop {
+  using IA = Img<T, AKO, BM>;
+  using IB = Img<T, BKO, BN>;
+  static constexpr int STAGE = IA::BYTES + IB::BYTES;
+  static constexpr int LDS_BYTES = 2 * STAGE;
+  static constexpr int TM = BM / 32, TN = BN / 32;  // MFMA tiles per wave (2x2 waves)
+  static_assert(IA::CHUNKS % 256 == 0 && IB::CHUNKS % 256 == 0, "tile/thread mismatch");
+
+  // Accumulates K-tiles [kt0, kt1) into acc. Caller zero-initialises acc.
+  template <class LA, class LB>
+  TT_DEV static void run(const LA& la, const LB& lb, int K, int kt0, int kt1, char* lds,
+                         f32x4 (&acc)[TM][TN]) {
+    if (kt0 >= kt1) return;
+    const int wave = threadIdx.x >> 6;
+    const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
+    uint4 ra[IA::CHUNKS / 256], rb[IB::CHUNKS / 256];
+    stage_load<T, AKO, BM>(la, kt0, K, ra);
+    stage_load<T, BKO, BN>(lb, kt0, K, rb);
+    stage_store<T, AKO, BM>(lds, ra);
+    stage_store<T, BKO, BN>(lds + IA::BYTES, rb);
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int cur = (kt - kt0) & 1;
+      const bool more = kt + 1 < kt1;
+      if (more) {
+        stage_load<T, AKO, BM>(la, kt + 1, K, ra);
+        stage_load<T, BKO, BN>(lb, kt + 1, K, rb);
+      }
+      const char* ia = lds + cur * STAGE;
+      const char* ib = ia + IA::BYTES;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        uint4 fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = frag<T, AKO>(ia, wm + 16 * i, ks);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = frag<T, BKO>(ib, wn + 16 * j, ks);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mma<T>(fa[i], fb[j], acc[i][j]);
+      }
+      if (more) {
+        char* nx = lds + (cur ^ 1) * STAGE;
+        stage_store<T, AKO, BM>(nx, ra);
+        stage_store<T, BKO, BN>(nx + IA::BYTES, rb);
+      }
+      __syncthreads();
+    }
+  }
+
+  // Visit every accumulator element as (tile_row, tile_col, value).
+  template <class F>
+  TT_DEV static void epilogue(const f32x4 (&acc)[TM][TN], F&& f) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          f(wm + 16 * i + 4 * (lane >> 4) + r, wn + 16 * j + (lane & 15), acc[i][j][r]);
+  }
+};
+
+// ---- common loaders ------------------------------------------------------------
+template <typename T>
+struct KCPlain {  // rows [r0, r0+ROWS) of a row-major [rows][ld] matrix
+  const T* base; long ld; int r0, rows;
+  TT_DEV const T* rowptr(int r) const { int g = r0 + r; return g < rows ? base + (long)g * ld : nullptr; }
+};
+template <typename T>
+struct KOPlain {  // columns [c0, c0+128) of a row-major [K][ld] matrix
+  const T* base; long ld; int c0, ncols;
+  TT_DEV const T* kptr(int k) const { return base + (long)k * ld + c0; }
+};
+// K-outer operand whose k index is (b*T + t) and whose source row is (b*T + t + shift),
+// zero when t+shift falls outside [0,T). Used for the GRU h_{s-1} operand of dW_hh.
+template <typename T>
+struct KOShift {
+  const T* base; long ld; int c0, ncols, T_, shift;
+  TT_DEV const T* kptr(int k) const {
+    const int t = k % T_;
+    const int ts = t + shift;
+    if (ts < 0 || ts >= T_) return nullptr;
+    return base + (long)(k + shift) * ld + c0;
+  }
+};
+
+}  // namespace ttg

@@ -1,0 +1,485 @@
+// Contrastive losses on the tower outputs: L2 normalisation, the fused in-batch
+// softmax cross-entropy (InfoNCE) over the B x N score matrix, hard-negative top-k
+// mining and the hinge (margin) loss over mined negatives.
+#include <algorithm>
+#include <float.h>
+
+#include "tt_api.h"
+#include "tt_gemm_core.h"
+
+namespace {
+
+constexpr int MAXC = 16;  // features per lane (h <= 1024)
+
+// ---------------------------------------------------------------- L2 normalise
+template <typename T>
+__global__ __launch_bounds__(256) void l2norm_fwd_kernel(const float* __restrict__ x, long rows, int C, float eps,
+                                                         T* __restrict__ y, float* __restrict__ y32,
+                                                         float* __restrict__ norm) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float v[MAXC];
+  float ss = 0.f;
+#pragma unroll
+  for (int q = 0; q < MAXC; ++q) {
+    const int c = lane + 64 * q;
+    v[q] = c < C ? x[row * C + c] : 0.f;
+    ss += v[q] * v[q];
+  }
+  const float nrm = sqrtf(wave_sum(ss));
+  const float inv = 1.f / fmaxf(nrm, eps);
+#pragma unroll
+  for (int q = 0; q < MAXC; ++q) {
+    const int c = lane + 64 * q;
+    if (c < C) {
+      Elt<T>::st(y + row * C + c, v[q] * inv);
+      if (y32) y32[row * C + c] = v[q] * inv;
+    }
+  }
+  if (lane == 0) norm[row] = nrm;
+}
+
+__global__ __launch_bounds__(256) void l2norm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                                         const float* __restrict__ norm, long rows, int C, float eps,
+                                                         float* __restrict__ dx, int accumulate) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float nrm = norm[row];
+  float g[MAXC], yy[MAXC];
+  float dot = 0.f;
+#pragma unroll
+  for (int q = 0; q < MAXC; ++q) {
+    const int c = lane + 64 * q;
+    g[q] = c < C ? dy[row * C + c] : 0.f;
+    yy[q] = c < C ? y[row * C + c] : 0.f;
+    dot += g[q] * yy[q];
+  }
+  dot = wave_sum(dot);
+  const bool clamped = !(nrm > eps);
+  const float inv = 1.f / fmaxf(nrm, eps);
+#pragma unroll
+  for (int q = 0; q < MAXC; ++q) {
+    const int c = lane + 64 * q;
+    if (c < C) {
+      const float d = clamped ? g[q] * inv : (g[q] - yy[q] * dot) * inv;
+      float* p = dx + row * C + c;
+      *p = accumulate ? *p + d : d;
+    }
+  }
+}
+
+// ----------------------------------------------------------- fused InfoNCE fwd
+// Grid (col_splits, row_blocks). Each workgroup sweeps its share of 128-column
+// dn tiles for 128 q rows, keeping a per-lane running (max, sum-exp) per row, and
+// writes one (max, sumexp) partial per row and split. S is never stored.
+template <typename T>
+__global__ __launch_bounds__(256) void infonce_fwd_kernel(const T* __restrict__ qn, long bq, const T* __restrict__ dn,
+                                                          long nd, int h, float inv_tau, float offdiag,
+                                                          long label_off, int ct_per_split, float* __restrict__ pm,
+                                                          float* __restrict__ pl, float* __restrict__ diag) {
+  using ML = ttg::MainLoop<T, false, false, 128, 128>;
+  __shared__ __attribute__((aligned(16))) char lds[ML::LDS_BYTES];
+  __shared__ float red_m[2][128], red_l[2][128];
+  const int m0 = blockIdx.y * 128;
+  const long nct = (nd + 127) / 128;
+  const long ct0 = (long)blockIdx.x * ct_per_split;
+  const long ct1 = std::min(nct, ct0 + ct_per_split);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int nk = (h * (int)sizeof(T) + ttg::KTB - 1) / ttg::KTB;
+  float rm[4][4], rl[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { rm[i][r] = -FLT_MAX; rl[i][r] = 0.f; }
+
+  for (long ct = ct0; ct < ct1; ++ct) {
+    const int n0 = (int)(ct * 128);
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    ML::run(ttg::KCPlain<T>{qn, h, m0, (int)bq}, ttg::KCPlain<T>{dn, h, n0, (int)nd}, h, 0, nk, lds, acc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long row = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
+        float sv[4];
+        float tmax = -FLT_MAX;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const long col = n0 + wn + 16 * j + (lane & 15);
+          float s = acc[i][j][r] * inv_tau;
+          const bool lab = (col == label_off + row);
+          if (!lab) s -= offdiag;
+          if (lab && row < bq) diag[row] = s;
+          if (col >= nd) s = -FLT_MAX;
+          sv[j] = s;
+          tmax = fmaxf(tmax, s);
+        }
+        const float nm = fmaxf(rm[i][r], tmax);
+        float l = rl[i][r] * __expf(rm[i][r] - nm);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) l += (sv[j] > -FLT_MAX) ? __expf(sv[j] - nm) : 0.f;
+        rm[i][r] = nm;
+        rl[i][r] = l;
+      }
+  }
+  // merge the 16 lanes sharing each row, then the two waves sharing it
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float M = max16(rm[i][r]);
+      const float L = sum16(rl[i][r] * __expf(rm[i][r] - M));
+      if ((lane & 15) == 0) {
+        const int rr = wm + 16 * i + 4 * (lane >> 4) + r;
+        red_m[wave & 1][rr] = M;
+        red_l[wave & 1][rr] = L;
+      }
+    }
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    const long row = m0 + threadIdx.x;
+    if (row < bq) {
+      const float a = red_m[0][threadIdx.x], b = red_m[1][threadIdx.x];
+      const float M = fmaxf(a, b);
+      const float L = red_l[0][threadIdx.x] * __expf(a - M) + red_l[1][threadIdx.x] * __expf(b - M);
+      pm[(long)blockIdx.x * bq + row] = M;
+      pl[(long)blockIdx.x * bq + row] = L;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void infonce_finalize_kernel(const float* __restrict__ pm,
+                                                               const float* __restrict__ pl, int splits, long bq,
+                                                               const float* __restrict__ diag, float* __restrict__ lse,
+                                                               float* __restrict__ row_loss) {
+  const long row = (long)blockIdx.x * 256 + threadIdx.x;
+  if (row >= bq) return;
+  float M = -FLT_MAX;
+  for (int s = 0; s < splits; ++s) M = fmaxf(M, pm[(long)s * bq + row]);
+  float L = 0.f;
+  for (int s = 0; s < splits; ++s) L += pl[(long)s * bq + row] * __expf(pm[(long)s * bq + row] - M);
+  const float v = M + __logf(L);
+  lse[row] = v;
+  row_loss[row] = v - diag[row];
+}
+
+// dS[i][j] = gscale * (softmax_ij - [j == label_i]) in dtype, full tiles.
+template <typename T>
+__global__ __launch_bounds__(256) void infonce_dscore_kernel(const T* __restrict__ qn, long bq,
+                                                             const T* __restrict__ dn, long nd, int h, float inv_tau,
+                                                             float offdiag, long label_off,
+                                                             const float* __restrict__ lse, float gscale,
+                                                             long ldds, T* __restrict__ ds) {
+  using ML = ttg::MainLoop<T, false, false, 128, 128>;
+  __shared__ __attribute__((aligned(16))) char lds[ML::LDS_BYTES];
+  const int m0 = blockIdx.y * 128, n0 = blockIdx.x * 128;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (h * (int)sizeof(T) + ttg::KTB - 1) / ttg::KTB;
+  ML::run(ttg::KCPlain<T>{qn, h, m0, (int)bq}, ttg::KCPlain<T>{dn, h, n0, (int)nd}, h, 0, nk, lds, acc);
+  ML::epilogue(acc, [&](int r, int c, float v) {
+    const long row = m0 + r, col = n0 + c;
+    if (row >= bq || col >= nd) return;
+    const bool lab = (col == label_off + row);
+    float s = v * inv_tau;
+    if (!lab) s -= offdiag;
+    const float p = __expf(s - lse[row]);
+    Elt<T>::st(ds + row * ldds + col, gscale * (p - (lab ? 1.f : 0.f)));
+  });
+}
+
+// -------------------------------------------------------------- top-k (k <= 8)
+// One wave per row: lane-local sorted top-k over columns lane, lane+64, ...
+// (ascending scan, strict '>' insertion keeps the lower column first on ties),
+// then k rounds of a wave arg-max with (value desc, index asc) ordering.
+constexpr int TOPK_MAX = 8;
+__global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict__ S, long rows, long cols,
+                                                        long label_off, int k, int32_t* __restrict__ idx,
+                                                        float* __restrict__ val) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float lv[TOPK_MAX];
+  int li[TOPK_MAX];
+#pragma unroll
+  for (int q = 0; q < TOPK_MAX; ++q) { lv[q] = -FLT_MAX; li[q] = 0x7fffffff; }
+  const float* sr = S + row * cols;
+  const long lab = label_off >= 0 ? label_off + row : -1;  // label_off < 0: nothing masked
+  for (long c = lane; c < cols; c += 64) {
+    float v = sr[c];
+    if (c == lab) v = -1.f;
+    if (v > lv[k - 1]) {
+      // insert keeping descending order; equal values stay ahead (lower column)
+      float cv = v;
+      int ci = (int)c;
+#pragma unroll
+      for (int q = 0; q < TOPK_MAX; ++q) {
+        if (q < k && cv > lv[q]) {
+          const float tv = lv[q];
+          const int ti = li[q];
+          lv[q] = cv;
+          li[q] = ci;
+          cv = tv;
+          ci = ti;
+        }
+      }
+    }
+  }
+  int head = 0;
+  for (int q = 0; q < k; ++q) {
+    float hv = -FLT_MAX;
+    int hi = 0x7fffffff;
+#pragma unroll
+    for (int p = 0; p < TOPK_MAX; ++p)
+      if (p == head) { hv = lv[p]; hi = li[p]; }
+    float bv = hv;
+    int bi = hi;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    if (lane == 0) {
+      idx[row * k + q] = bi;
+      if (val) val[row * k + q] = bv;
+    }
+    if (hi == bi && head < TOPK_MAX) ++head;
+  }
+}
+
+// ---------------------------------------------------------------- margin loss
+__global__ __launch_bounds__(256) void margin_fwd_kernel(const float* __restrict__ qn, long bq,
+                                                         const float* __restrict__ dn, int h, long label_off,
+                                                         const int32_t* __restrict__ idx, int k, float margin,
+                                                         float* __restrict__ row_loss) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= bq) return;
+  const float* q = qn + row * h;
+  const float* dp = dn + (label_off + row) * h;
+  float pos = 0.f, neg = 0.f;
+  for (int c = lane; c < h; c += 64) pos += q[c] * dp[c];
+  for (int j = 0; j < k; ++j) {
+    const float* dj = dn + (long)idx[row * k + j] * h;
+    for (int c = lane; c < h; c += 64) neg += q[c] * dj[c];
+  }
+  pos = wave_sum(pos);
+  neg = wave_sum(neg) / k;
+  if (lane == 0) row_loss[row] = fmaxf(margin - pos + neg, 0.f);
+}
+
+__global__ __launch_bounds__(256) void margin_bwd_kernel(const float* __restrict__ qn, long bq,
+                                                         const float* __restrict__ dn, int h, long label_off,
+                                                         const int32_t* __restrict__ idx, int k, float margin,
+                                                         float gscale, float* __restrict__ dqn,
+                                                         float* __restrict__ ddn) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= bq) return;
+  const float* q = qn + row * h;
+  const long lab = label_off + row;
+  const float* dp = dn + lab * h;
+  float pos = 0.f, neg = 0.f;
+  for (int c = lane; c < h; c += 64) pos += q[c] * dp[c];
+  for (int j = 0; j < k; ++j) {
+    const float* dj = dn + (long)idx[row * k + j] * h;
+    for (int c = lane; c < h; c += 64) neg += q[c] * dj[c];
+  }
+  pos = wave_sum(pos);
+  neg = wave_sum(neg) / k;
+  // torch.clamp(min=0) passes the gradient where the argument is >= 0
+  const bool active = (margin - pos + neg) >= 0.f;
+  const float gn = active ? gscale / k : 0.f;
+  const float gp = active ? -gscale : 0.f;
+  for (int c = lane; c < h; c += 64) {
+    float d = gp * dp[c];
+    for (int j = 0; j < k; ++j) d += gn * dn[(long)idx[row * k + j] * h + c];
+    dqn[row * h + c] = d;
+  }
+  if (active) {
+    for (int c = lane; c < h; c += 64) {
+      atomicAdd(ddn + lab * h + c, gp * q[c]);
+      for (int j = 0; j < k; ++j) atomicAdd(ddn + (long)idx[row * k + j] * h + c, gn * q[c]);
+    }
+  }
+}
+
+inline int esize(int dtype) { return dtype == TT_DT_BF16 ? 2 : 4; }
+
+struct InfoWs {
+  long ds, sk;
+};
+inline long infonce_ws(int dtype, long bq, long nd, int h, InfoWs* w) {
+  auto al = [](long x) { return (x + 255) & ~255L; };
+  const int s1 = tt_gemm_pick_splits((int)bq, h, (int)nd, 1);
+  const int s2 = tt_gemm_pick_splits((int)nd, h, (int)bq, 1);
+  const long sk = std::max(tt_gemm_ws_size((int)bq, h, 1, s1), tt_gemm_ws_size((int)nd, h, 1, s2));
+  w->ds = 0;
+  w->sk = al(bq * ((nd + 7) / 8 * 8) * esize(dtype));
+  return w->sk + al(sk * 4);
+}
+
+}  // namespace
+
+extern "C" int tt_l2norm_fwd(int dtype, const float* x, long rows, int cols, float eps, void* y, float* y32,
+                             float* norm, void* stream) {
+  TT_CHECK_ARG(cols <= 64 * MAXC, "tt_l2norm_fwd: cols %d > %d", cols, 64 * MAXC);
+  if (rows == 0) return 0;
+  dim3 g((unsigned)tt_ceil_div(rows, 4));
+  if (dtype == TT_DT_BF16)
+    hipLaunchKernelGGL(l2norm_fwd_kernel<bf16_t>, g, dim3(256), 0, (hipStream_t)stream, x, rows, cols, eps,
+                       (bf16_t*)y, y32, norm);
+  else
+    hipLaunchKernelGGL(l2norm_fwd_kernel<float>, g, dim3(256), 0, (hipStream_t)stream, x, rows, cols, eps,
+                       (float*)y, y32, norm);
+  TT_CHECK_LAUNCH("l2norm_fwd_kernel");
+  return 0;
+}
+
+extern "C" int tt_l2norm_bwd(const float* dy, const float* y32, const float* norm, long rows, int cols, float eps,
+                             float* dx, int accumulate, void* stream) {
+  TT_CHECK_ARG(cols <= 64 * MAXC, "tt_l2norm_bwd: cols %d", cols);
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(l2norm_bwd_kernel, dim3((unsigned)tt_ceil_div(rows, 4)), dim3(256), 0, (hipStream_t)stream, dy,
+                     y32, norm, rows, cols, eps, dx, accumulate);
+  TT_CHECK_LAUNCH("l2norm_bwd_kernel");
+  return 0;
+}
+
+extern "C" long tt_infonce_fwd_ws_size(long bq, long nd) {
+  const int rb = tt_ceil_div(bq, 128);
+  const long nct = (nd + 127) / 128;
+  const long splits = std::max<long>(1, std::min<long>(nct, tt_ceil_div(1024, rb)));
+  return (2L * splits * bq + bq) * (long)sizeof(float);
+}
+
+extern "C" int tt_infonce_fwd(int dtype, const void* qn, long bq, const void* dn, long nd, int h, float inv_tau,
+                              float offdiag_sub, long label_offset, float* lse, float* row_loss, void* ws,
+                              void* stream) {
+  TT_CHECK_ARG(dtype == TT_DT_F32 || dtype == TT_DT_BF16, "tt_infonce_fwd: bad dtype");
+  TT_CHECK_ARG(label_offset >= 0 && label_offset + bq <= nd, "tt_infonce_fwd: labels outside [0, nd)");
+  TT_CHECK_ARG((h * esize(dtype)) % 16 == 0, "tt_infonce_fwd: h=%d misaligned", h);
+  TT_CHECK_ARG(bq <= 65535L * 128 && nd < (1L << 31), "tt_infonce_fwd: too large");
+  if (bq == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const int rb = tt_ceil_div(bq, 128);
+  const long nct = (nd + 127) / 128;
+  int splits = (int)std::max<long>(1, std::min<long>(nct, tt_ceil_div(1024, rb)));
+  const int per = tt_ceil_div(nct, splits);
+  splits = tt_ceil_div(nct, per);
+  TT_CHECK_ARG(ws != nullptr, "tt_infonce_fwd: null workspace");
+  float* pool = static_cast<float*>(ws);
+  float* pm = pool;
+  float* pl = pool + (long)splits * bq;
+  float* diag = pl + (long)splits * bq;
+  dim3 grid(splits, rb);
+  if (dtype == TT_DT_BF16)
+    hipLaunchKernelGGL(infonce_fwd_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)qn, bq, (const bf16_t*)dn,
+                       nd, h, inv_tau, offdiag_sub, label_offset, per, pm, pl, diag);
+  else
+    hipLaunchKernelGGL(infonce_fwd_kernel<float>, grid, dim3(256), 0, st, (const float*)qn, bq, (const float*)dn, nd,
+                       h, inv_tau, offdiag_sub, label_offset, per, pm, pl, diag);
+  TT_CHECK_LAUNCH("infonce_fwd_kernel");
+  hipLaunchKernelGGL(infonce_finalize_kernel, dim3(tt_ceil_div(bq, 256)), dim3(256), 0, st, pm, pl, splits, bq, diag,
+                     lse, row_loss);
+  TT_CHECK_LAUNCH("infonce_finalize_kernel");
+  return 0;
+}
+
+extern "C" long tt_infonce_bwd_ws_size(int dtype, long bq, long nd, int h) {
+  InfoWs w;
+  return infonce_ws(dtype, bq, nd, h, &w);
+}
+
+extern "C" int tt_infonce_bwd(int dtype, const void* qn, long bq, const void* dn, long nd, int h, float inv_tau,
+                              float offdiag_sub, long label_offset, const float* lse, float gscale, float* dqn,
+                              float* ddn, void* ws, void* stream) {
+  TT_CHECK_ARG(dtype == TT_DT_F32 || dtype == TT_DT_BF16, "tt_infonce_bwd: bad dtype");
+  TT_CHECK_ARG(label_offset >= 0 && label_offset + bq <= nd, "tt_infonce_bwd: labels outside [0, nd)");
+  if (bq == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  InfoWs w;
+  infonce_ws(dtype, bq, nd, h, &w);
+  char* base = static_cast<char*>(ws);
+  void* ds = base + w.ds;
+  float* sk = reinterpret_cast<float*>(base + w.sk);
+  const long ldds = (nd + 7) / 8 * 8;  // 16-byte aligned rows for the dS operand
+  dim3 grid((unsigned)tt_ceil_div(nd, 128), (unsigned)tt_ceil_div(bq, 128));
+  if (dtype == TT_DT_BF16)
+    hipLaunchKernelGGL(infonce_dscore_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)qn, bq,
+                       (const bf16_t*)dn, nd, h, inv_tau, offdiag_sub, label_offset, lse, gscale, ldds, (bf16_t*)ds);
+  else
+    hipLaunchKernelGGL(infonce_dscore_kernel<float>, grid, dim3(256), 0, st, (const float*)qn, bq, (const float*)dn,
+                       nd, h, inv_tau, offdiag_sub, label_offset, lse, gscale, ldds, (float*)ds);
+  TT_CHECK_LAUNCH("infonce_dscore_kernel");
+  // dqn = inv_tau * dS dn   (NN)
+  {
+    tt_gemm_batch g{};
+    g.a[0] = ds; g.b[0] = dn; g.c[0] = dqn;
+    const int sp = tt_gemm_pick_splits((int)bq, h, (int)nd, 1);
+    TT_PROPAGATE(tt_gemm(dtype, TT_DT_F32, 0, 1, (int)bq, h, (int)nd, &g, 1, ldds, h, h, inv_tau, 0, 0, 0, 0, 0.f, sp,
+                         sk, stream));
+  }
+  // ddn = inv_tau * dS^T qn (TN)
+  {
+    tt_gemm_batch g{};
+    g.a[0] = ds; g.b[0] = qn; g.c[0] = ddn;
+    const int sp = tt_gemm_pick_splits((int)nd, h, (int)bq, 1);
+    TT_PROPAGATE(tt_gemm(dtype, TT_DT_F32, 1, 1, (int)nd, h, (int)bq, &g, 1, ldds, h, h, inv_tau, 0, 0, 0, 0, 0.f, sp,
+                         sk, stream));
+  }
+  return 0;
+}
+
+extern "C" long tt_hardneg_ws_size(int dtype, long bq, long nd) {
+  (void)dtype;
+  return bq * nd * 4;
+}
+
+extern "C" int tt_hardneg_topk(int dtype, const void* qn, long bq, const void* dn, long nd, int h, long label_offset,
+                               int k, int32_t* idx, float* val, void* ws, void* stream) {
+  TT_CHECK_ARG(k >= 1 && k <= TOPK_MAX && k < nd, "tt_hardneg_topk: k=%d", k);
+  TT_CHECK_ARG(label_offset < 0 || label_offset + bq <= nd, "tt_hardneg_topk: labels outside [0, nd)");
+  if (bq == 0) return 0;
+  float* S = static_cast<float*>(ws);
+  tt_gemm_batch g{};
+  g.a[0] = qn; g.b[0] = dn; g.c[0] = S;
+  TT_PROPAGATE(tt_gemm(dtype, TT_DT_F32, 0, 0, (int)bq, (int)nd, h, &g, 1, h, h, nd, 1.f, 0, 0, 0, 0, 0.f, 1,
+                       nullptr, stream));
+  hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)tt_ceil_div(bq, 4)), dim3(256), 0, (hipStream_t)stream, S, bq,
+                     nd, label_offset, k, idx, val);
+  TT_CHECK_LAUNCH("topk_rows_kernel");
+  return 0;
+}
+
+extern "C" int tt_margin_fwd(const float* qn, long bq, const float* dn, long nd, int h, long label_offset,
+                             const int32_t* idx, int k, float margin, float* row_loss, void* stream) {
+  TT_CHECK_ARG(label_offset >= 0 && label_offset + bq <= nd && k >= 1, "tt_margin_fwd: bad labels/k");
+  if (bq == 0) return 0;
+  hipLaunchKernelGGL(margin_fwd_kernel, dim3((unsigned)tt_ceil_div(bq, 4)), dim3(256), 0, (hipStream_t)stream, qn, bq,
+                     dn, h, label_offset, idx, k, margin, row_loss);
+  TT_CHECK_LAUNCH("margin_fwd_kernel");
+  return 0;
+}
+
+extern "C" int tt_margin_bwd(const float* qn, long bq, const float* dn, long nd, int h, long label_offset,
+                             const int32_t* idx, int k, float margin, float gscale, float* dqn, float* ddn,
+                             void* stream) {
+  TT_CHECK_ARG(label_offset >= 0 && label_offset + bq <= nd && k >= 1, "tt_margin_bwd: bad labels/k");
+  if (bq == 0) return 0;
+  hipLaunchKernelGGL(margin_bwd_kernel, dim3((unsigned)tt_ceil_div(bq, 4)), dim3(256), 0, (hipStream_t)stream, qn, bq,
+                     dn, h, label_offset, idx, k, margin, gscale, dqn, ddn);
+  TT_CHECK_LAUNCH("margin_bwd_kernel");
+  return 0;
+}

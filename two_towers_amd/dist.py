@@ -1,0 +1,84 @@
+"""Data-parallel plumbing: one process per GPU, torch.distributed over RCCL ("nccl").
+
+The reference has no parallelism. The DP step here:
+  forward : all-gather the normalised doc vectors so every rank scores its queries
+            against the global negative pool (labels offset by rank * B_local);
+  backward: reduce-scatter (sum) the gradient wrt the gathered doc vectors back to the
+            rank that owns each row; all-reduce (sum) the parameter gradients.
+Each rank's loss is its rows' share of the GLOBAL mean (divided by the global batch),
+so the summed gradients are exactly the single-process gradients of the whole batch.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def active(group=None) -> bool:
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+
+
+def rank_world(group=None):
+    if not active(group):
+        return 0, 1
+    return dist.get_rank(group), dist.get_world_size(group)
+
+
+def all_gather_rows(x: torch.Tensor, group=None) -> torch.Tensor:
+    """[B_l, ...] on every rank -> [world * B_l, ...] in rank order (no autograd)."""
+    r, w = rank_world(group)
+    if w == 1:
+        return x
+    out = torch.empty((w * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x.contiguous(), group=group)
+    return out
+
+
+def reduce_scatter_rows(x: torch.Tensor, group=None) -> torch.Tensor:
+    """[world * B_l, ...] partial sums on every rank -> this rank's [B_l, ...] total."""
+    r, w = rank_world(group)
+    if w == 1:
+        return x
+    out = torch.empty((x.shape[0] // w,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.reduce_scatter_tensor(out, x.contiguous(), op=dist.ReduceOp.SUM, group=group)
+    return out
+
+
+def all_reduce_sum_(t: torch.Tensor, group=None):
+    if active(group):
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t
+
+
+class GatherRows(torch.autograd.Function):
+    """Differentiable all-gather: backward reduce-scatters the gradient."""
+
+    @staticmethod
+    def forward(ctx, x, group):
+        ctx.group = group
+        return all_gather_rows(x, group)
+
+    @staticmethod
+    def backward(ctx, g):
+        return reduce_scatter_rows(g, ctx.group), None
+
+
+def allreduce_grads(params, group=None, bucket_bytes: int = 64 << 20):
+    """Sum parameter gradients across ranks in flat buckets (one collective per
+    ~64 MB bucket: xGMI rings are per-link bound, so few large collectives win)."""
+    if not active(group):
+        return
+    grads = [p.grad for p in params if p.grad is not None]
+    bucket, size = [], 0
+    for g in grads + [None]:
+        if g is not None:
+            bucket.append(g)
+            size += g.numel() * g.element_size()
+        if bucket and (g is None or size >= bucket_bytes):
+            flat = torch.cat([b.reshape(-1) for b in bucket])
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+            off = 0
+            for b in bucket:
+                b.copy_(flat[off:off + b.numel()].view_as(b))
+                off += b.numel()
+            bucket, size = [], 0

@@ -1,0 +1,59 @@
+"""Adam for the inner loop of train_enhanced.py:43,63 as one multi-tensor HIP launch.
+
+Same hyper-parameters and update formula as torch.optim.Adam (non-amsgrad,
+non-maximize); state lives in fp32 tensors per parameter ('exp_avg', 'exp_avg_sq',
+'step' like torch, so optimizer.state_dict() keeps torch's structure).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import call, stream_ptr
+
+_MAXT = 48
+
+
+class Adam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        if lr < 0.0 or eps < 0.0 or not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0:
+            raise ValueError("invalid Adam hyper-parameter")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            ps = [p for p in group["params"] if p.grad is not None]
+            if not ps:
+                continue
+            _lib.require_gpu(*ps)
+            b1, b2 = group["betas"]
+            # torch keeps one step counter per parameter; parameters stepped together share it
+            buckets = {}
+            for p in ps:
+                st = self.state[p]
+                if not st:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                if p.dtype != torch.float32 or not p.is_contiguous() or not p.grad.is_contiguous():
+                    raise _lib.TTError("two_towers_amd Adam expects contiguous fp32 parameters and gradients")
+                st["step"] += 1
+                buckets.setdefault(int(st["step"].item()), []).append(p)
+            for step, plist in buckets.items():
+                for i in range(0, len(plist), _MAXT):
+                    chunk = plist[i:i + _MAXT]
+                    n = len(chunk)
+                    arr = lambda xs: (ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])
+                    sizes = (ctypes.c_long * n)(*[p.numel() for p in chunk])
+                    call("tt_adam_multi", arr(chunk), arr([p.grad for p in chunk]),
+                         arr([self.state[p]["exp_avg"] for p in chunk]),
+                         arr([self.state[p]["exp_avg_sq"] for p in chunk]), sizes, n, group["lr"], b1, b2,
+                         group["eps"], group["weight_decay"], step, stream_ptr(chunk[0].device))
+        return loss

@@ -1,0 +1,323 @@
+"""Forward/backward of one or two encoder towers on the HIP path.
+
+A tower is the reference's encoder: nn.GRU(E, 2h, num_layers=2, bidirectional,
+dropout=0.1) followed by Linear(4h,2h) -> LayerNorm -> ReLU -> Linear(2h,h)
+(enhanced_two_tower.py:17-48, :50-60). The query and doc towers of
+EnhancedTwoTowerModel.forward (:62-65) run through the same kernel launches: every
+GEMM is batched over towers (and directions) and every GRU step launch covers all
+four recurrences.
+
+Layout in HBM (per tower; row = b*T + t, dt = compute dtype):
+  X0  [B*T, Ep]  dt   layer-0 input (gathered Word2Vec rows / packed floats)
+  G   [B*T, 6H]  dt   input projections, fwd gates r|z|n then rev gates
+  Y   [B*T, 2H]  dt   layer output h_t (fwd | rev), X1 = dropout(Y0) (layer-1 input)
+  S   [B*T, 4H]  dt   saved pre-activations of r|z|n and gh_n per direction
+  dG, dGH [B*T, 6H] dt  gradients wrt gate pre-activations (input / hidden side)
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib, ops
+from ._lib import GruBwdRec, GruFwdRec, HeadBwdIO, HeadFwdIO, call, dtype_code, stream_ptr
+
+PARAMS_PER_TOWER = 22
+LN_EPS = 1e-5
+
+
+def gru_param_names():
+    names = []
+    for layer in (0, 1):
+        for sfx in ("", "_reverse"):
+            for w in ("weight_ih", "weight_hh", "bias_ih", "bias_hh"):
+                names.append(f"{w}_l{layer}{sfx}")
+    return names
+
+
+GRU_NAMES = gru_param_names()
+HEAD_NAMES = ["0.weight", "0.bias", "1.weight", "1.bias", "3.weight", "3.bias"]
+
+
+@dataclass(frozen=True)
+class TowerCfg:
+    ntowers: int
+    E: int
+    H: int  # GRU hidden per direction (= 2 * hidden_dim)
+    h: int  # output dim (= hidden_dim)
+    dtype: torch.dtype
+    drop_p: float  # dropout between GRU layers (0 in eval)
+
+
+class _Packed:
+    """Per-step compute-dtype copies of one tower's weights in the kernels' layouts."""
+
+    def __init__(self, p, cfg: TowerCfg, Ep: int):
+        dt, H, E = cfg.dtype, cfg.H, cfg.E
+        g = dict(zip(GRU_NAMES, p[:16]))
+        hd = dict(zip(HEAD_NAMES, p[16:]))
+        self.wih = []
+        self.bias = []
+        self.whh = []
+        self.bhn = []
+        for layer in (0, 1):
+            wf, wr = g[f"weight_ih_l{layer}"], g[f"weight_ih_l{layer}_reverse"]
+            w = torch.cat([wf, wr], 0)
+            if layer == 0 and Ep != E:
+                w = F.pad(w, (0, Ep - E))
+            self.wih.append(w.to(dt).contiguous())
+            bs = []
+            for sfx in ("", "_reverse"):
+                bi, bh = g[f"bias_ih_l{layer}{sfx}"], g[f"bias_hh_l{layer}{sfx}"]
+                bs.append(torch.cat([bi[: 2 * H] + bh[: 2 * H], bi[2 * H:]]))
+            self.bias.append(torch.cat(bs).float().contiguous())
+            self.whh.append([g[f"weight_hh_l{layer}{s}"].to(dt).contiguous() for s in ("", "_reverse")])
+            self.bhn.append([g[f"bias_hh_l{layer}{s}"][2 * H:].float().contiguous() for s in ("", "_reverse")])
+        self.w1 = hd["0.weight"].to(dt).contiguous()
+        self.b1 = hd["0.bias"].float().contiguous()
+        self.ln_g = hd["1.weight"].float().contiguous()
+        self.ln_b = hd["1.bias"].float().contiguous()
+        self.w2 = hd["3.weight"].to(dt).contiguous()
+        self.b2 = hd["3.bias"].float().contiguous()
+
+
+def _alloc(shape, dt, dev):
+    return torch.empty(shape, dtype=dt, device=dev)
+
+
+def featurize(x: torch.Tensor, table: torch.Tensor | None, Ep: int, dt: torch.dtype) -> torch.Tensor:
+    """[B,T] ids -> gathered rows, or [B,T,E] floats -> packed rows; returns [B*T, Ep]."""
+    if x.dtype in (torch.int32, torch.int64):
+        if table is None:
+            raise _lib.TTError("integer token ids need an embedding table (model.set_embedding_table)")
+        if table.dtype != dt or table.shape[1] != Ep:
+            raise _lib.TTError(f"embedding table must be {dt} with {Ep} columns, got {table.dtype} {tuple(table.shape)}")
+        ids = x.reshape(-1).to(torch.int32).contiguous()
+        out = _alloc((ids.numel(), Ep), dt, x.device)
+        ops.embed_gather(table, ids, out)
+        return out
+    if x.dim() != 3:
+        raise ValueError(f"expected [B, T, E] embeddings or [B, T] token ids, got shape {tuple(x.shape)}")
+    src = x.float().contiguous()
+    out = _alloc((src.shape[0] * src.shape[1], Ep), dt, x.device)
+    ops.pack_rows(src, out)
+    return out
+
+
+def _gru_layer_fwd(cfg, xs, K, ldx, packs, layer, B, T, seeds, want_x1):
+    n, H, dt, dev = cfg.ntowers, cfg.H, cfg.dtype, xs[0].device
+    BT = B * T
+    G = [_alloc((BT, 6 * H), dt, dev) for _ in range(n)]
+    ops.gemm(xs, [p.wih[layer] for p in packs], G, m=BT, n=6 * H, k=K, lda=ldx, ldb=K, ldc=6 * H,
+             a_kouter=False, b_kouter=False, dtype=dt, out_dtype=dt, bias=[p.bias[layer] for p in packs])
+    Y = [_alloc((BT, 2 * H), dt, dev) for _ in range(n)]
+    X1 = [_alloc((BT, 2 * H), dt, dev) for _ in range(n)] if want_x1 else None
+    S = [[_alloc((BT, 4 * H), dt, dev) for _ in range(2)] for _ in range(n)]
+    hs = _alloc((n * 2, 2, B, H), torch.float32, dev)
+    recs = (GruFwdRec * (2 * n))()
+    for ti in range(n):
+        for d in range(2):
+            r = recs[ti * 2 + d]
+            r.g = G[ti][:, d * 3 * H:].data_ptr()
+            r.whh = packs[ti].whh[layer][d].data_ptr()
+            r.bhn = packs[ti].bhn[layer][d].data_ptr()
+            r.y = Y[ti][:, d * H:].data_ptr()
+            r.x1 = X1[ti][:, d * H:].data_ptr() if want_x1 else None
+            r.save = S[ti][d].data_ptr()
+            r.hstate = hs[ti * 2 + d].data_ptr()
+            r.dir = d
+            r.drop_seed = seeds[ti] & 0xFFFFFFFF
+            r.drop_col0 = d * H
+    call("tt_gru_fwd", dtype_code(dt), recs, 2 * n, B, T, H, 6 * H, 2 * H, cfg.drop_p if want_x1 else 0.0,
+         stream_ptr(dev))
+    del G
+    return Y, X1, S
+
+
+def _gru_layer_bwd(cfg, layer, B, T, S, Y, dY, dfinal, packs):
+    """Returns dG, dGH ([B*T, 6H] per tower) and bias grads (dbih, dbhh per tower/dir)."""
+    n, H, dt, dev = cfg.ntowers, cfg.H, cfg.dtype, Y[0].device
+    BT = B * T
+    lib = _lib.load()
+    dG = [_alloc((BT, 6 * H), dt, dev) for _ in range(n)]
+    dGH = [_alloc((BT, 6 * H), dt, dev) for _ in range(n)]
+    dhs = _alloc((n * 2, 2, B, H), torch.float32, dev)
+    nbr = lib.tt_gru_bias_rows(B)
+    part = _alloc((n * 2, nbr, 4 * H), torch.float32, dev)
+    recs = (GruBwdRec * (2 * n))()
+    for ti in range(n):
+        for d in range(2):
+            r = recs[ti * 2 + d]
+            r.save = S[ti][d].data_ptr()
+            r.y = Y[ti][:, d * H:].data_ptr()
+            r.dy = dY[ti][:, d * H:].data_ptr() if dY is not None else None
+            r.dfinal = dfinal[ti][:, d * H:].data_ptr() if dfinal is not None else None
+            r.whh = packs[ti].whh[layer][d].data_ptr()
+            r.dgx = dG[ti][:, d * 3 * H:].data_ptr()
+            r.dgh = dGH[ti][:, d * 3 * H:].data_ptr()
+            r.dhstate = dhs[ti * 2 + d].data_ptr()
+            r.dbias_part = part[ti * 2 + d].data_ptr()
+            r.dir = d
+    ldf = dfinal[0].shape[1] if dfinal is not None else 0
+    call("tt_gru_bwd", dtype_code(dt), recs, 2 * n, B, T, H, 2 * H, 6 * H, ldf, stream_ptr(dev))
+    sums = _alloc((n * 2, 4 * H), torch.float32, dev)
+    for i in range(2 * n):
+        ops.colsum(part[i], nbr, 4 * H, 4 * H, sums[i])
+    dbih = [[sums[ti * 2 + d, : 3 * H] for d in range(2)] for ti in range(n)]
+    dbhh = [[torch.cat([sums[ti * 2 + d, : 2 * H], sums[ti * 2 + d, 3 * H:]]) for d in range(2)] for ti in range(n)]
+    return dG, dGH, dbih, dbhh
+
+
+def _weight_grads(cfg, B, T, dG, dGH, Xin, K, ldx, Y):
+    """dW_ih = dG^T Xin, dW_hh = dGH^T Y_{t-1} for all (tower, dir) in two batched TN GEMMs."""
+    n, H, dt, dev = cfg.ntowers, cfg.H, cfg.dtype, dG[0].device
+    BT = B * T
+    dWih = [[_alloc((3 * H, K), torch.float32, dev) for _ in range(2)] for _ in range(n)]
+    dWhh = [[_alloc((3 * H, H), torch.float32, dev) for _ in range(2)] for _ in range(n)]
+    a_ih, b_ih, c_ih, a_hh, b_hh, c_hh, sh = [], [], [], [], [], [], []
+    for ti in range(n):
+        for d in range(2):
+            a_ih.append(dG[ti][:, d * 3 * H:])
+            b_ih.append(Xin[ti])
+            c_ih.append(dWih[ti][d])
+            a_hh.append(dGH[ti][:, d * 3 * H:])
+            b_hh.append(Y[ti][:, d * H:])
+            c_hh.append(dWhh[ti][d])
+            sh.append(-1 if d == 0 else 1)
+    ops.gemm(a_ih, b_ih, c_ih, m=3 * H, n=K, k=BT, lda=6 * H, ldb=ldx, ldc=K, a_kouter=True, b_kouter=True,
+             dtype=dt, out_dtype=torch.float32)
+    ops.gemm(a_hh, b_hh, c_hh, m=3 * H, n=H, k=BT, lda=6 * H, ldb=2 * H, ldc=H, a_kouter=True, b_kouter=True,
+             dtype=dt, out_dtype=torch.float32, bshift=sh, seq_t=T)
+    return dWih, dWhh
+
+
+class TowersFn(torch.autograd.Function):
+    """(x_0..x_{n-1}, params...) -> (vec_0..vec_{n-1}), vec_i = tower_i(x_i) as [B, h] fp32."""
+
+    @staticmethod
+    def forward(ctx, cfg: TowerCfg, table, *args):
+        n = cfg.ntowers
+        xs, params = args[:n], args[n:]
+        _lib.require_gpu(*xs, *params)
+        dt, E, H, h = cfg.dtype, cfg.E, cfg.H, cfg.h
+        dev = xs[0].device
+        B, T = xs[0].shape[0], xs[0].shape[1]
+        for x in xs:
+            if x.shape[0] != B or x.shape[1] != T:
+                raise ValueError("query and doc inputs must share [B, T] in one fused call")
+        Ep = ops.pad_cols(E, dt)
+        packs = [_Packed(params[i * PARAMS_PER_TOWER:(i + 1) * PARAMS_PER_TOWER], cfg, Ep) for i in range(n)]
+        X0 = [featurize(x, table, Ep, dt) for x in xs]
+        train_drop = cfg.drop_p > 0.0
+        seeds = [int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) for _ in range(n)] if train_drop else [0] * n
+        Y0, X1, S0 = _gru_layer_fwd(cfg, X0, Ep, Ep, packs, 0, B, T, seeds, train_drop)
+        Xl1 = X1 if train_drop else Y0
+        Y1, _, S1 = _gru_layer_fwd(cfg, Xl1, 2 * H, 2 * H, packs, 1, B, T, seeds, False)
+        # cat(h_fwd at t=T-1, h_rev at t=0) -> [B, 2H] (enhanced_two_tower.py:53,59)
+        hcat = []
+        for ti in range(n):
+            y = Y1[ti].view(B, T, 2 * H)
+            hcat.append(torch.cat([y[:, T - 1, :H], y[:, 0, H:]], 1).contiguous())
+        outs, p1s, means, rstds, us = [], [], [], [], []
+        io = (HeadFwdIO * n)()
+        for ti in range(n):
+            pk = packs[ti]
+            p1 = _alloc((B, 2 * h), dt, dev)
+            u = _alloc((B, 2 * h), dt, dev)
+            mean = _alloc((B,), torch.float32, dev)
+            rstd = _alloc((B,), torch.float32, dev)
+            out = _alloc((B, h), torch.float32, dev)
+            q = io[ti]
+            q.w1, q.b1, q.ln_g, q.ln_b = pk.w1.data_ptr(), pk.b1.data_ptr(), pk.ln_g.data_ptr(), pk.ln_b.data_ptr()
+            q.w2, q.b2 = pk.w2.data_ptr(), pk.b2.data_ptr()
+            q.x, q.p1, q.mean, q.rstd, q.u, q.out = (hcat[ti].data_ptr(), p1.data_ptr(), mean.data_ptr(),
+                                                     rstd.data_ptr(), u.data_ptr(), out.data_ptr())
+            outs.append(out); p1s.append(p1); means.append(mean); rstds.append(rstd); us.append(u)
+        call("tt_proj_head_fwd", dtype_code(dt), io, n, B, h, LN_EPS, stream_ptr(dev))
+        ctx.cfg = cfg
+        ctx.dims = (B, T, Ep)
+        ctx.seeds = seeds
+        ctx.packs = packs
+        ctx.acts = (X0, Y0, X1, S0, Y1, S1, hcat, p1s, means, rstds, us)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        cfg = ctx.cfg
+        n, dt, E, H, h = cfg.ntowers, cfg.dtype, cfg.E, cfg.H, cfg.h
+        B, T, Ep = ctx.dims
+        packs = ctx.packs
+        X0, Y0, X1, S0, Y1, S1, hcat, p1s, means, rstds, us = ctx.acts
+        dev = Y0[0].device
+        lib = _lib.load()
+        st = stream_ptr(dev)
+        # ---- projection head
+        head_grads = []
+        dhcat = []
+        ws = _alloc((lib.tt_proj_head_bwd_ws_size(dtype_code(dt), B, h),), torch.uint8, dev)
+        for ti in range(n):
+            g = gouts[ti]
+            g = torch.zeros(B, h, dtype=torch.float32, device=dev) if g is None else g.float().contiguous()
+            pk = packs[ti]
+            dx = _alloc((B, 2 * H), torch.float32, dev)
+            dw1 = _alloc(pk.w1.shape, torch.float32, dev)
+            db1 = _alloc((2 * h,), torch.float32, dev)
+            dg = _alloc((2 * h,), torch.float32, dev)
+            dbeta = _alloc((2 * h,), torch.float32, dev)
+            dw2 = _alloc(pk.w2.shape, torch.float32, dev)
+            db2 = _alloc((h,), torch.float32, dev)
+            io = HeadBwdIO()
+            io.w1, io.ln_g, io.ln_b, io.w2 = pk.w1.data_ptr(), pk.ln_g.data_ptr(), pk.ln_b.data_ptr(), pk.w2.data_ptr()
+            io.x, io.p1, io.mean, io.rstd, io.u = (hcat[ti].data_ptr(), p1s[ti].data_ptr(), means[ti].data_ptr(),
+                                                   rstds[ti].data_ptr(), us[ti].data_ptr())
+            io.dout, io.dx = g.data_ptr(), dx.data_ptr()
+            io.dw1, io.db1, io.dg, io.dbeta, io.dw2, io.db2 = (dw1.data_ptr(), db1.data_ptr(), dg.data_ptr(),
+                                                               dbeta.data_ptr(), dw2.data_ptr(), db2.data_ptr())
+            io.ws = ws.data_ptr()
+            call("tt_proj_head_bwd", dtype_code(dt), ctypes.byref(io), 1, B, h, LN_EPS, st)
+            head_grads.append([dw1, db1, dg, dbeta, dw2, db2])
+            dhcat.append(dx)
+        # ---- GRU layer 1: dfinal enters at the last processed step of each direction
+        dG1, dGH1, dbih1, dbhh1 = _gru_layer_bwd(cfg, 1, B, T, S1, Y1, None, dhcat, packs)
+        Xl1 = X1 if X1 is not None else Y0
+        dWih1, dWhh1 = _weight_grads(cfg, B, T, dG1, dGH1, Xl1, 2 * H, 2 * H, Y1)
+        # dL/dY0 = (dG1 Wih1) * dropout mask  [B*T, 2H]
+        dY0 = [_alloc((B * T, 2 * H), dt, dev) for _ in range(n)]
+        if X1 is None:
+            ops.gemm(dG1, [p.wih[1] for p in packs], dY0, m=B * T, n=2 * H, k=6 * H, lda=6 * H, ldb=2 * H,
+                     ldc=2 * H, a_kouter=False, b_kouter=True, dtype=dt, out_dtype=dt)
+        else:
+            for ti in range(n):
+                ops.gemm([dG1[ti]], [packs[ti].wih[1]], [dY0[ti]], m=B * T, n=2 * H, k=6 * H, lda=6 * H, ldb=2 * H,
+                         ldc=2 * H, a_kouter=False, b_kouter=True, dtype=dt, out_dtype=dt, drop_seed=ctx.seeds[ti],
+                         drop_p=cfg.drop_p)
+        del dG1, dGH1
+        # ---- GRU layer 0
+        dG0, dGH0, dbih0, dbhh0 = _gru_layer_bwd(cfg, 0, B, T, S0, Y0, dY0, None, packs)
+        del dY0
+        dWih0, dWhh0 = _weight_grads(cfg, B, T, dG0, dGH0, X0, Ep, Ep, Y0)
+        grads = []
+        for ti in range(n):
+            gl = {}
+            for layer, (dWih, dWhh, dbih, dbhh) in enumerate(((dWih0, dWhh0, dbih0, dbhh0),
+                                                               (dWih1, dWhh1, dbih1, dbhh1))):
+                for d, sfx in enumerate(("", "_reverse")):
+                    w = dWih[ti][d]
+                    if layer == 0 and Ep != E:
+                        w = w[:, :E].contiguous()
+                    gl[f"weight_ih_l{layer}{sfx}"] = w
+                    gl[f"weight_hh_l{layer}{sfx}"] = dWhh[ti][d]
+                    gl[f"bias_ih_l{layer}{sfx}"] = dbih[ti][d].contiguous()
+                    gl[f"bias_hh_l{layer}{sfx}"] = dbhh[ti][d]
+            grads.extend(gl[k] for k in GRU_NAMES)
+            grads.extend(head_grads[ti])
+        ctx.acts = None
+        ctx.packs = None
+        return (None, None, *([None] * n), *grads)
+
+
+def run_towers(cfg: TowerCfg, table, xs, params):
+    return TowersFn.apply(cfg, table, *xs, *params)

@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""Training-throughput benchmark of the two-tower step on MI355X (driver contract).
+
+One step = the train_enhanced.py inner loop (train_enhanced.py:54-69) on one batch of
+synthetic token ids already resident in HBM: Word2Vec gather -> 2 x 2-layer BiGRU
+-> projection heads -> hard-negative mining (k=5) + margin loss (0.2) -> backward ->
+gradient all-reduce (N>1) -> Adam. Workload = BASELINE.json configs[2]
+(EnhancedTwoTowerModel(300, 256), seq_len 64, batch 8192 per GPU, bf16); with N GPUs
+the job is data-parallel with the doc embeddings all-gathered (configs[3] at N=8),
+i.e. weak scaling at 8192 pairs per rank.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line. `roofline` is measured live with HIP events around the
+dominant kernel's launches; `cpu_baseline` times the CPU oracle (oracle/cpu_ref.py,
+PyTorch-CPU, same model/loss) on a bounded sample on this host's cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+
+import torch
+import torch.distributed as tdist
+
+METRIC = "training pairs/sec at global batch=8192, 1/2/4/8 GPUs; MRR@10 match"
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BF16_PEAK_TFS = 2500.0    # dense bf16 MFMA (no sparsity)
+FP32_PEAK_TFS = 157.3     # fp32 MFMA = vector rate
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=8192, help="pairs per GPU")
+    ap.add_argument("--seq", type=int, default=64)
+    ap.add_argument("--hidden", type=int, default=256)
+    ap.add_argument("--emb", type=int, default=300)
+    ap.add_argument("--vocab", type=int, default=3_000_000)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--loss", default="hardneg_margin", choices=["hardneg_margin", "infonce"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=256, help="pairs per CPU-baseline step")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--timing", action="store_true", help="print the per-kernel HIP-event table to stderr")
+    return ap.parse_args()
+
+
+def make_batches(n, B, T, V, gen, device):
+    """Uniform ids in [0, V) with a 10% pad tail per row (-1 -> zero rows), like
+    EnhancedDataset padding of short texts (enhanced_two_tower.py:160-162)."""
+    out = []
+    pad = max(1, T // 10)
+    for _ in range(n):
+        q = torch.randint(0, V, (B, T), generator=gen, dtype=torch.int64).to(torch.int32)
+        d = torch.randint(0, V, (B, T), generator=gen, dtype=torch.int64).to(torch.int32)
+        q[:, T - pad:] = -1
+        d[:, T - pad:] = -1
+        out.append((q.to(device), d.to(device)))
+    return out
+
+
+def cpu_baseline(args):
+    """The CPU oracle (PyTorch-CPU restatement of the reference, fp32) on a bounded
+    sample of the same workload: same model size, seq_len, loss; smaller batch."""
+    import numpy as np
+
+    from oracle import cpu_ref
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    torch.set_num_threads(threads)
+    E, h, T, B = args.emb, args.hidden, args.seq, args.cpu_batch
+    p = {k: v.clone().requires_grad_(True) for k, v in cpu_ref.counter_params(E, h, 0).items()}
+    opt = torch.optim.Adam(list(p.values()))
+    rng = np.random.default_rng(0)
+    table = torch.from_numpy((rng.standard_normal((20000, E)) * 0.1).astype(np.float32))
+
+    def batch():
+        ids = torch.from_numpy(rng.integers(0, table.shape[0], (2, B, T)))
+        x = table[ids]
+        x[:, :, T - max(1, T // 10):] = 0
+        return x[0], x[1]
+
+    def step():
+        q, d = batch()  # host gather as in EnhancedDataset
+        opt.zero_grad()
+        qv, dv = cpu_ref.forward(q, d, p, drop_p=0.1, seeds=(1, 2))
+        if args.loss == "infonce":
+            loss = cpu_ref.infonce(qv, dv)
+        else:
+            with torch.no_grad():
+                s = cpu_ref.normalize(qv, 1e-8) @ cpu_ref.normalize(dv, 1e-8).t()
+                s.fill_diagonal_(-1.0)
+                idx = s.topk(5, dim=1).indices
+            loss = cpu_ref.margin_loss(qv, dv, dv[idx.reshape(-1)])
+        loss.backward()
+        opt.step()
+
+    step()  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        step()
+    dt = time.perf_counter() - t0
+    return {"value": round(B * args.cpu_steps / dt, 2), "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/cpu_ref.py fp32 train step (fwd+{args.loss}+bwd+Adam), E={E} h={h} T={T}, "
+                      f"batch {B} x {args.cpu_steps} timed steps after 1 warm-up ({dt:.1f} s), "
+                      f"torch {torch.__version__} CPU, {threads} threads"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    group = None
+    if world > 1:
+        tdist.init_process_group("nccl", device_id=dev)
+    import two_towers_amd as tta
+    from two_towers_amd import dist as tdp
+    from two_towers_amd import timing
+
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    B, T, h, E, V = args.batch, args.seq, args.hidden, args.emb, args.vocab
+    torch.manual_seed(1234)  # same weights on every rank
+    model = tta.EnhancedTwoTowerModel(E, h).to(dev).set_compute_dtype(dt).train()
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    table = (torch.randn(V, E, device=dev, generator=gen) * 0.1).to(dt)  # Word2Vec-shaped, resident in HBM
+    model.set_embedding_table(table)
+    del table
+    cpu_gen = torch.Generator().manual_seed(99 + rank)
+    batches = make_batches(4, B, T, V, cpu_gen, dev)
+    if args.loss == "infonce":
+        crit = tta.InfoNCELoss(compute_dtype=dt, process_group=group)
+    else:
+        crit = tta.HardNegativeMarginLoss(k=5, margin=0.2, compute_dtype=dt, process_group=group)
+    opt = tta.Adam(model.parameters(), lr=1e-3)
+    params = list(model.parameters())
+
+    def step(i):
+        q, d = batches[i % len(batches)]
+        opt.zero_grad(set_to_none=True)
+        qv, dv = model(q, d)
+        loss = crit(qv, dv)
+        loss.backward()
+        tdp.allreduce_grads(params, group)
+        opt.step()
+        return loss
+
+    for i in range(args.warmup):
+        loss = step(i)
+    first_loss = float(loss) if args.warmup else float("nan")
+    if world > 1:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    timing.reset()
+    timing.enabled = True
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        tdist.barrier()
+    elapsed = time.perf_counter() - t0
+    timing.enabled = False
+    kt = timing.summary()
+    final_loss = float(loss)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    pairs = B * world * args.steps
+    value = pairs / elapsed
+
+    # Roofline of the dominant kernel (largest device time inside the timed region).
+    peak = BF16_PEAK_TFS if dt == torch.bfloat16 else FP32_PEAK_TFS
+    flop_regions = {k: v for k, v in kt.items() if k not in ("embed_gather",)}
+    dom = max(flop_regions, key=lambda k: flop_regions[k]["ms_total"])
+    r = kt[dom]
+    achieved = r["work"] / (r["ms_total"] * 1e-3) / 1e12
+    roofline = {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": None,
+                "work_per_launch": r["work_per_launch"], "ms_per_launch": round(r["ms_per_launch"], 5)}
+    extra = {}
+    if "embed_gather" in kt:
+        g = kt["embed_gather"]
+        gbs = g["work"] / (g["ms_total"] * 1e-3) / 1e9
+        extra["embed_gather"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(gbs / HBM_PEAK_GBS, 4), "ms_per_launch": round(g["ms_per_launch"], 5)}
+    for name in ("hardneg_topk", "infonce_fwd"):
+        if name in kt:
+            g = kt[name]
+            tfs = g["work"] / (g["ms_total"] * 1e-3) / 1e12
+            extra[name] = {"bound": "mfma", "achieved": round(tfs, 2), "peak": peak, "unit": "TFLOP/s",
+                           "frac": round(tfs / peak, 4), "ms_per_launch": round(g["ms_per_launch"], 5)}
+    step_ms = 1e3 * elapsed / args.steps
+    kernels = {k: {"ms_per_step": round(v["ms_total"] / args.steps, 3),
+                   "tflops": round(v["work"] / (v["ms_total"] * 1e-3) / 1e12, 1) if k != "embed_gather" else None}
+               for k, v in sorted(kt.items(), key=lambda kv: -kv[1]["ms_total"])}
+    if args.timing and rank == 0:
+        import sys
+        print(json.dumps(kernels, indent=1), file=sys.stderr)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": args.dtype,
+            "data": f"synthetic: uniform token ids over a {V}x{E} Word2Vec-shaped table resident in HBM, "
+                    f"10% pad tail per row, random-init weights (torch seed 1234)",
+            "config": {"workload": ("BASELINE configs[2]: EnhancedTwoTowerModel(300, 256), seq_len 64, "
+                                    "batch 8192 per GPU, hard-negative mining k=5 + margin 0.2, dropout 0.1, Adam"
+                                    if args.loss == "hardneg_margin" else
+                                    "EnhancedTwoTowerModel(300, 256), seq_len 64, batch 8192 per GPU, InfoNCE"),
+                       "global_batch": B * world, "seq_len": T, "hidden": h, "embedding_dim": E,
+                       "parallelism": f"dp{world}", "loss": args.loss},
+            "roofline": roofline,
+            "rooflines_secondary": extra,
+            "kernel_ms_per_step": kernels,
+            "loss_first_last": [round(first_loss, 5), round(final_loss, 5)],
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

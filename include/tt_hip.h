@@ -191,7 +191,7 @@ long tt_infonce_bwd_ws_size(int dtype, long bq, long nd, int h);
 
 /* Hard-negative mining, batched over rows (get_hard_negatives,
  * enhanced_two_tower.py:123-133): sims = qn dn^T (cosine for normalised inputs), the
- * positive column label_offset+i set to -1 (label_offset < 0: no column masked), top-k (k <= 8) indices per row sorted by
+ * positive column label_offset+i set to -1 (label_offset < 0: no column masked), top-k (k <= 16) indices per row sorted by
  * descending similarity; ties broken towards the lower column index.
  * idx [bq, k] int32, val [bq, k] fp32 (optional). ws: tt_hardneg_ws_size bytes. */
 int tt_hardneg_topk(int dtype, const void* qn, long bq, const void* dn, long nd, int h,

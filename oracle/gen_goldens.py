@@ -37,7 +37,7 @@ def import_reference():
 
 
 def sd_arrays(prefix, sd):
-    return {f"{prefix}{k}": v.detach().cpu().numpy() for k, v in sd.items()}
+    return {f"{prefix}{k}": v.detach().cpu().numpy().copy() for k, v in sd.items()}  # copy: .numpy() aliases
 
 
 class FakeW2V(dict):

@@ -1,0 +1,80 @@
+"""Data-parallel host logic (two_towers_amd/dist.py) at world_size 2 over gloo on CPU.
+
+The loss math here is the oracle's (CPU); what is under test is the DP plumbing the
+GPU path uses unchanged: GatherRows (all-gather forward / reduce-scatter backward),
+the global-mean loss split, and the bucketed gradient all-reduce. Two ranks holding
+half a batch each must reproduce the single-process gradients of the whole batch."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from oracle import cpu_ref
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _dp_loss(p, q, d, group, rank, world):
+    from two_towers_amd import dist as tdp
+    qv, dv = cpu_ref.forward(q, d, p)
+    qn, dn = cpu_ref.normalize(qv), cpu_ref.normalize(dv)
+    dn_all = tdp.GatherRows.apply(dn.contiguous(), group)
+    B = q.shape[0]
+    s = qn @ dn_all.t() / 0.07
+    labels = torch.arange(B) + rank * B
+    local_sum = torch.nn.functional.cross_entropy(s, labels, reduction="sum")
+    loss = local_sum / (B * world)
+    tot = loss.detach().clone()
+    tdp.all_reduce_sum_(tot, group)
+    return loss + (tot - loss.detach())
+
+
+def _worker(rank, world, port, q, d, p0, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    from two_towers_amd import dist as tdp
+    B = q.shape[0] // world
+    p = {k: v.clone().requires_grad_(True) for k, v in p0.items()}
+    loss = _dp_loss(p, q[rank * B:(rank + 1) * B], d[rank * B:(rank + 1) * B], None, rank, world)
+    loss.backward()
+    params = list(p.values())
+    for t in params:
+        t.grad = t.grad.contiguous()
+    tdp.allreduce_grads(params, None, bucket_bytes=4096)
+    if rank == 0:
+        out.put((float(loss.detach()), {k: v.grad.numpy().copy() for k, v in p.items()}))  # by value
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_dp_gather_loss_and_grads_match_single_process(world):
+    torch.manual_seed(0)
+    p0 = cpu_ref.counter_params(12, 8, 3)
+    g = torch.Generator().manual_seed(4)
+    q = torch.randn(16, 5, 12, generator=g)
+    d = torch.randn(16, 5, 12, generator=g)
+    ref_p = {k: v.clone().requires_grad_(True) for k, v in p0.items()}
+    ref_loss = cpu_ref.infonce(*cpu_ref.forward(q, d, ref_p))
+    ref_loss.backward()
+    ctx = mp.get_context("spawn")
+    out = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, d, p0, out)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    loss, grads = out.get(timeout=120)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert abs(loss - float(ref_loss)) < 1e-5
+    for k, v in ref_p.items():
+        torch.testing.assert_close(torch.from_numpy(grads[k]), v.grad, rtol=1e-4, atol=1e-6)

@@ -1,0 +1,123 @@
+"""Host-side logic on CPU: module surface, featurisation, data formats, C-ABI exports,
+and that the product path refuses to run without the GPU."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+import two_towers_amd as tta
+from oracle import cpu_ref
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def test_state_dict_matches_reference_layout():
+    m = tta.EnhancedTwoTowerModel(300, 256)
+    ref = cpu_ref.reference_param_shapes(300, 256)
+    sd = m.state_dict()
+    assert sorted(sd) == sorted(ref) and len(sd) == 44
+    for k, shp in ref.items():
+        assert tuple(sd[k].shape) == shp, k
+    assert sum(v.numel() for v in sd.values()) == 15_764_992
+    assert tta.EnhancedTwoTower is tta.EnhancedTwoTowerModel
+
+
+def test_same_init_as_reference_for_same_seed():
+    # tiny_model.npz holds the reference's weights for torch.manual_seed(0), (16, 8)
+    z = np.load(os.path.join(GOLD, "tiny_model.npz"))
+    torch.manual_seed(0)
+    m = tta.EnhancedTwoTowerModel(16, 8)
+    for k, v in m.state_dict().items():
+        np.testing.assert_array_equal(v.numpy(), z[f"w.{k}"], err_msg=k)
+
+
+def test_enhanced_dataset_and_ids_match_reference():
+    z = np.load(os.path.join(GOLD, "featurize.npz"))
+    words = [str(w) for w in z["words"]]
+    w2v = {w: z["vecs"][i] for i, w in enumerate(words)}
+
+    class KV(dict):
+        vector_size = z["vecs"].shape[1]
+
+    T = int(z["max_length"])
+    texts = [str(t) for t in z["texts"]]
+    ds = tta.EnhancedDataset(texts, texts, KV(w2v), max_length=T)
+    vocab = tta.Vocab(words, z["vecs"])
+    for i, t in enumerate(texts):
+        np.testing.assert_array_equal(ds[i][0].numpy(), z["emb"][i])
+        ids = tta.encode_ids(t, vocab, T)
+        assert len(ids) == T
+        np.testing.assert_array_equal(cpu_ref.ids_to_embedding(ids, z["vecs"]), z["emb"][i])
+
+
+def test_vocab_roundtrip(tmp_path):
+    v = tta.Vocab(["a", "b", "c"], np.arange(6, dtype=np.float32).reshape(3, 2))
+    path = str(tmp_path / "w2v.npz")
+    v.save(path)
+    w = tta.Vocab.load(path)
+    assert w.index == v.index
+    np.testing.assert_array_equal(w.vectors, v.vectors)
+    assert tta.encode_ids("B zzz a", w, 4) == [1, 0, -1, -1]
+    assert tta.encode_ids("zzz", w, 3) == [-1, -1, -1]
+
+
+def test_msmarco_pairing_rule():
+    samples = [
+        {"query": "q1", "passages": {"passage_text": ["p1", "p2", "p3"], "is_selected": [0, 1, 1]}},
+        {"query": "", "passages": {"passage_text": ["x"], "is_selected": [1]}},
+        {"query": "q3"},
+        {"query": "q4", "passages": {"passage_text": ["p4"], "is_selected": [0]}},
+    ]
+    assert tta.pairs_from_msmarco(samples) == (["q1", "q1"], ["p2", "p3"])
+
+
+def header_functions():
+    text = open(os.path.join(ROOT, "include", "tt_hip.h")).read()
+    return sorted(set(re.findall(r"^(?:int|long|const char\*)\s+(tt_\w+)\(", text, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    from two_towers_amd import _lib
+    lib = _lib.load()
+    names = header_functions()
+    assert len(names) >= 25
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(names) == set(_lib.EXPORTED), set(names) ^ set(_lib.EXPORTED)
+    assert lib.tt_version().decode().startswith("tt_hip")
+
+
+def test_bad_arguments_are_reported_not_launched():
+    from two_towers_amd import _lib
+    lib = _lib.load()
+    rc = lib.tt_gemm(7, 0, 0, 0, 4, 4, 4, None, 1, 4, 4, 4, 1.0, 0, 0, 0, 0, 0.0, 1, None, None)
+    assert rc == _lib.TT_EINVAL
+    assert "dtype" in lib.tt_last_error().decode()
+    assert lib.tt_adam_multi(None, None, None, None, None, 0, 1e-3, 0.9, 0.999, 1e-8, 0.0, 0, None) == _lib.TT_EINVAL
+
+
+def test_product_path_fails_loudly_without_gpu():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    m = tta.EnhancedTwoTowerModel(16, 8)
+    with pytest.raises(RuntimeError, match="GPU"):
+        m(torch.randn(2, 3, 16), torch.randn(2, 3, 16))
+    with pytest.raises(RuntimeError, match="GPU"):
+        tta.InfoNCELoss()(torch.randn(4, 8), torch.randn(4, 8))
+    with pytest.raises(RuntimeError, match="GPU"):
+        tta.get_hard_negatives(torch.randn(8), torch.randn(10, 8), 0)
+
+
+def test_oracle_is_not_imported_by_the_product():
+    import ast
+    pkg = os.path.join(ROOT, "two_towers_amd")
+    for f in os.listdir(pkg):
+        if f.endswith(".py"):
+            tree = ast.parse(open(os.path.join(pkg, f)).read())
+            for node in ast.walk(tree):
+                if isinstance(node, (ast.Import, ast.ImportFrom)):
+                    mods = [a.name for a in node.names] if isinstance(node, ast.Import) else [node.module or ""]
+                    assert not any(m.startswith("oracle") for m in mods), f

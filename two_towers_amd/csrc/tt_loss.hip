@@ -198,11 +198,11 @@ __global__ __launch_bounds__(256) void infonce_dscore_kernel(const T* __restrict
   });
 }
 
-// -------------------------------------------------------------- top-k (k <= 8)
+// ------------------------------------------------------------- top-k (k <= 16)
 // One wave per row: lane-local sorted top-k over columns lane, lane+64, ...
 // (ascending scan, strict '>' insertion keeps the lower column first on ties),
 // then k rounds of a wave arg-max with (value desc, index asc) ordering.
-constexpr int TOPK_MAX = 8;
+constexpr int TOPK_MAX = 16;
 __global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict__ S, long rows, long cols,
                                                         long label_off, int k, int32_t* __restrict__ idx,
                                                         float* __restrict__ val) {

@@ -45,9 +45,11 @@ class EnhancedTwoTowerModel(nn.Module):
 
     def set_embedding_table(self, table: torch.Tensor | None):
         """Attach a device Word2Vec table [V, E] (any float dtype); token-id inputs then
-        gather rows on the GPU. Stored padded in the compute dtype."""
+        gather rows on the GPU. Stored padded in the compute dtype (built on first use;
+        the source tensor may be dropped after that)."""
         if table is None:
             self._table = None
+            self._table_src = None
             return self
         if table.dim() != 2 or table.shape[1] != self.embedding_dim:
             raise ValueError(f"table must be [V, {self.embedding_dim}]")
@@ -65,6 +67,7 @@ class EnhancedTwoTowerModel(nn.Module):
         if t is None or t.dtype != dt or t.device != device or t.shape[1] != ep:
             t = torch.zeros(src.shape[0], ep, dtype=dt, device=device)
             t[:, : self.embedding_dim] = src.to(device=device, dtype=dt)
+            t.real_cols = self.embedding_dim  # for algorithmic-byte accounting (timing.py)
             self._table = t
         return t
 

@@ -1,0 +1,46 @@
+"""Optional live kernel timing with HIP events (used by bench.py).
+
+Events are recorded on torch's current stream, which is the stream every libtt_hip
+launch is issued on (the ops pass torch.cuda.current_stream()). A region records its
+launch count and algorithmic work (FLOPs or bytes) so rooflines can be computed
+from measured device time.
+"""
+from __future__ import annotations
+
+from collections import defaultdict
+from contextlib import contextmanager
+
+import torch
+
+enabled = False
+_records = defaultdict(list)
+
+
+def reset():
+    _records.clear()
+
+
+@contextmanager
+def region(name: str, launches: int, work: float):
+    if not enabled:
+        yield
+        return
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
+    yield
+    e.record()
+    _records[name].append((s, e, launches, work))
+
+
+def summary():
+    """name -> dict(ms_total, launches, work, ms_per_launch, work_per_launch). Synchronises."""
+    torch.cuda.synchronize()
+    out = {}
+    for name, recs in _records.items():
+        ms = sum(s.elapsed_time(e) for s, e, _, _ in recs)
+        n = sum(r[2] for r in recs)
+        w = sum(r[3] for r in recs)
+        out[name] = dict(ms_total=ms, launches=n, work=w, ms_per_launch=ms / max(n, 1),
+                         work_per_launch=w / max(n, 1), calls=len(recs))
+    return out

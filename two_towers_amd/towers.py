@@ -22,7 +22,7 @@ from dataclasses import dataclass
 import torch
 import torch.nn.functional as F
 
-from . import _lib, ops
+from . import _lib, ops, timing
 from ._lib import GruBwdRec, GruFwdRec, HeadBwdIO, HeadFwdIO, call, dtype_code, stream_ptr
 
 PARAMS_PER_TOWER = 22
@@ -88,6 +88,10 @@ def _alloc(shape, dt, dev):
     return torch.empty(shape, dtype=dt, device=dev)
 
 
+def table_cols(table, x):
+    return getattr(table, "real_cols", table.shape[1])
+
+
 def featurize(x: torch.Tensor, table: torch.Tensor | None, Ep: int, dt: torch.dtype) -> torch.Tensor:
     """[B,T] ids -> gathered rows, or [B,T,E] floats -> packed rows; returns [B*T, Ep]."""
     if x.dtype in (torch.int32, torch.int64):
@@ -97,7 +101,10 @@ def featurize(x: torch.Tensor, table: torch.Tensor | None, Ep: int, dt: torch.dt
             raise _lib.TTError(f"embedding table must be {dt} with {Ep} columns, got {table.dtype} {tuple(table.shape)}")
         ids = x.reshape(-1).to(torch.int32).contiguous()
         out = _alloc((ids.numel(), Ep), dt, x.device)
-        ops.embed_gather(table, ids, out)
+        esz = 2 if dt == torch.bfloat16 else 4
+        # algorithmic bytes per row: id + the E real columns read and written
+        with timing.region("embed_gather", 1, ids.numel() * (4 + 2 * table_cols(table, x) * esz)):
+            ops.embed_gather(table, ids, out)
         return out
     if x.dim() != 3:
         raise ValueError(f"expected [B, T, E] embeddings or [B, T] token ids, got shape {tuple(x.shape)}")
@@ -111,8 +118,9 @@ def _gru_layer_fwd(cfg, xs, K, ldx, packs, layer, B, T, seeds, want_x1):
     n, H, dt, dev = cfg.ntowers, cfg.H, cfg.dtype, xs[0].device
     BT = B * T
     G = [_alloc((BT, 6 * H), dt, dev) for _ in range(n)]
-    ops.gemm(xs, [p.wih[layer] for p in packs], G, m=BT, n=6 * H, k=K, lda=ldx, ldb=K, ldc=6 * H,
-             a_kouter=False, b_kouter=False, dtype=dt, out_dtype=dt, bias=[p.bias[layer] for p in packs])
+    with timing.region(f"input_proj_l{layer}", 1, 2.0 * BT * 6 * H * K * n):
+        ops.gemm(xs, [p.wih[layer] for p in packs], G, m=BT, n=6 * H, k=K, lda=ldx, ldb=K, ldc=6 * H,
+                 a_kouter=False, b_kouter=False, dtype=dt, out_dtype=dt, bias=[p.bias[layer] for p in packs])
     Y = [_alloc((BT, 2 * H), dt, dev) for _ in range(n)]
     X1 = [_alloc((BT, 2 * H), dt, dev) for _ in range(n)] if want_x1 else None
     S = [[_alloc((BT, 4 * H), dt, dev) for _ in range(2)] for _ in range(n)]
@@ -131,8 +139,9 @@ def _gru_layer_fwd(cfg, xs, K, ldx, packs, layer, B, T, seeds, want_x1):
             r.dir = d
             r.drop_seed = seeds[ti] & 0xFFFFFFFF
             r.drop_col0 = d * H
-    call("tt_gru_fwd", dtype_code(dt), recs, 2 * n, B, T, H, 6 * H, 2 * H, cfg.drop_p if want_x1 else 0.0,
-         stream_ptr(dev))
+    with timing.region("gru_fwd_step", T, 2.0 * B * H * 3 * H * 2 * n * (T - 1)):
+        call("tt_gru_fwd", dtype_code(dt), recs, 2 * n, B, T, H, 6 * H, 2 * H, cfg.drop_p if want_x1 else 0.0,
+             stream_ptr(dev))
     del G
     return Y, X1, S
 
@@ -162,7 +171,8 @@ def _gru_layer_bwd(cfg, layer, B, T, S, Y, dY, dfinal, packs):
             r.dbias_part = part[ti * 2 + d].data_ptr()
             r.dir = d
     ldf = dfinal[0].shape[1] if dfinal is not None else 0
-    call("tt_gru_bwd", dtype_code(dt), recs, 2 * n, B, T, H, 2 * H, 6 * H, ldf, stream_ptr(dev))
+    with timing.region("gru_bwd_step", T, 2.0 * B * 3 * H * H * 2 * n * (T - 1)):
+        call("tt_gru_bwd", dtype_code(dt), recs, 2 * n, B, T, H, 2 * H, 6 * H, ldf, stream_ptr(dev))
     sums = _alloc((n * 2, 4 * H), torch.float32, dev)
     for i in range(2 * n):
         ops.colsum(part[i], nbr, 4 * H, 4 * H, sums[i])
@@ -187,10 +197,12 @@ def _weight_grads(cfg, B, T, dG, dGH, Xin, K, ldx, Y):
             b_hh.append(Y[ti][:, d * H:])
             c_hh.append(dWhh[ti][d])
             sh.append(-1 if d == 0 else 1)
-    ops.gemm(a_ih, b_ih, c_ih, m=3 * H, n=K, k=BT, lda=6 * H, ldb=ldx, ldc=K, a_kouter=True, b_kouter=True,
-             dtype=dt, out_dtype=torch.float32)
-    ops.gemm(a_hh, b_hh, c_hh, m=3 * H, n=H, k=BT, lda=6 * H, ldb=2 * H, ldc=H, a_kouter=True, b_kouter=True,
-             dtype=dt, out_dtype=torch.float32, bshift=sh, seq_t=T)
+    with timing.region("wgrad_ih", 1, 2.0 * 3 * H * K * BT * 2 * n):
+        ops.gemm(a_ih, b_ih, c_ih, m=3 * H, n=K, k=BT, lda=6 * H, ldb=ldx, ldc=K, a_kouter=True, b_kouter=True,
+                 dtype=dt, out_dtype=torch.float32)
+    with timing.region("wgrad_hh", 1, 2.0 * 3 * H * H * BT * 2 * n):
+        ops.gemm(a_hh, b_hh, c_hh, m=3 * H, n=H, k=BT, lda=6 * H, ldb=2 * H, ldc=H, a_kouter=True, b_kouter=True,
+                 dtype=dt, out_dtype=torch.float32, bshift=sh, seq_t=T)
     return dWih, dWhh
 
 
@@ -286,14 +298,15 @@ class TowersFn(torch.autograd.Function):
         dWih1, dWhh1 = _weight_grads(cfg, B, T, dG1, dGH1, Xl1, 2 * H, 2 * H, Y1)
         # dL/dY0 = (dG1 Wih1) * dropout mask  [B*T, 2H]
         dY0 = [_alloc((B * T, 2 * H), dt, dev) for _ in range(n)]
-        if X1 is None:
-            ops.gemm(dG1, [p.wih[1] for p in packs], dY0, m=B * T, n=2 * H, k=6 * H, lda=6 * H, ldb=2 * H,
-                     ldc=2 * H, a_kouter=False, b_kouter=True, dtype=dt, out_dtype=dt)
-        else:
-            for ti in range(n):
-                ops.gemm([dG1[ti]], [packs[ti].wih[1]], [dY0[ti]], m=B * T, n=2 * H, k=6 * H, lda=6 * H, ldb=2 * H,
-                         ldc=2 * H, a_kouter=False, b_kouter=True, dtype=dt, out_dtype=dt, drop_seed=ctx.seeds[ti],
-                         drop_p=cfg.drop_p)
+        with timing.region("dgrad_l1", 1, 2.0 * B * T * 2 * H * 6 * H * n):
+            if X1 is None:
+                ops.gemm(dG1, [p.wih[1] for p in packs], dY0, m=B * T, n=2 * H, k=6 * H, lda=6 * H, ldb=2 * H,
+                         ldc=2 * H, a_kouter=False, b_kouter=True, dtype=dt, out_dtype=dt)
+            else:
+                for ti in range(n):
+                    ops.gemm([dG1[ti]], [packs[ti].wih[1]], [dY0[ti]], m=B * T, n=2 * H, k=6 * H, lda=6 * H,
+                             ldb=2 * H, ldc=2 * H, a_kouter=False, b_kouter=True, dtype=dt, out_dtype=dt,
+                             drop_seed=ctx.seeds[ti], drop_p=cfg.drop_p)
         del dG1, dGH1
         # ---- GRU layer 0
         dG0, dGH0, dbih0, dbhh0 = _gru_layer_bwd(cfg, 0, B, T, S0, Y0, dY0, None, packs)

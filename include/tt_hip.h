@@ -112,7 +112,8 @@ int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B, int T, in
 
 /* Backward (BPTT) of tt_gru_fwd. Produces dL/dg (= dgx, feeds dWih, dbih and the
  * layer-input gradient) and dL/dgh (feeds dWhh), plus per-tile bias partial sums
- * (columns r|z|n|ghn, reduce with tt_colsum: dbih = [0:3H], dbhh = [0:2H],[3H:4H]). */
+ * (one row per 128-row batch tile; columns r|z|n|ghn; reduce with tt_colsum:
+ * dbih = [0:3H], dbhh = [0:2H] ++ [3H:4H]). */
 typedef struct {
   const void* save;    /* [B*T, 4H] from tt_gru_fwd          */
   const void* y;       /* layer output (source of h_{s-1})   */
@@ -121,7 +122,7 @@ typedef struct {
   const void* whh;     /* [3H, H]                            */
   void* dgx;           /* [B*T, ldd]                         */
   void* dgh;           /* [B*T, ldd]                         */
-  float* dhstate;      /* fp32 scratch [2][B][H]             */
+  float* dhstate;      /* fp32 scratch [2][B][H] (carry dh*z)  */
   float* dbias_part;   /* fp32 [tt_gru_bias_rows(B)][4H]; zeroed by tt_gru_bwd */
   int dir;
 } tt_gru_bwd_rec;

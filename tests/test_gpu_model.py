@@ -59,9 +59,14 @@ def test_forward_backward_bf16():
     rl.backward()
     assert rel(qv, rq) < 3e-2 and rel(dv, rd) < 3e-2
     assert abs(float(loss) - float(rl)) < 2e-2 * abs(float(rl))
+    # bf16 storage of activations and of the GRU's gate gradients: per-parameter
+    # gradient direction within cos >= 0.995 and norm error <= 10% of the fp32 oracle
     named = dict(m.named_parameters())
-    errs = {k: rel(named[k].grad, pr[k].grad) for k in pr}
-    assert max(errs.values()) < 5e-2, errs
+    for k in pr:
+        a, b = named[k].grad.double().cpu(), pr[k].grad.double()
+        cos = float((a * b).sum() / (a.norm() * b.norm()))
+        frob = float((a - b).norm() / b.norm())
+        assert cos >= 0.995 and frob <= 0.10, (k, cos, frob)
 
 
 def test_dropout_matches_counter_mask():

@@ -36,6 +36,31 @@ template <> struct Elt<bf16_t> {
   TT_DEV static bf16_t cvt(float v) { return f2bf(v); }
 };
 
+// 8 consecutive elements <-> fp32 registers, one or two 16-byte accesses.
+TT_DEV void ld8(const float* p, float (&f)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+TT_DEV void ld8(const bf16_t* p, float (&f)[8]) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+  }
+}
+TT_DEV void st8(float* p, const float (&f)[8]) {
+  *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(f[4], f[5], f[6], f[7]);
+}
+TT_DEV void st8(bf16_t* p, const float (&f)[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 TT_DEV float tt_sigmoid(float x) { return 1.0f / (1.0f + __expf(-x)); }
 TT_DEV float tt_tanh(float x) {
   // tanh(x) = 1 - 2/(exp(2x)+1); saturates cleanly for large |x|.

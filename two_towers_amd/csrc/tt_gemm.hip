@@ -34,6 +34,7 @@ struct GemmArgs {
   uint32_t drop_seed, drop_thresh;
   float drop_inv_keep;
   long part_stride;  // elements between split partials (fp32), 0 if no split
+  int vec_ok;        // C rows 16-byte aligned: 8-column vector stores allowed
 };
 
 constexpr int BM = 128, BN = 128;
@@ -76,27 +77,73 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     run(ttg::KCPlain<T>{A, g.lda, m0, g.M});
   }
 
-  if (g.splits > 1) {
-    float* P = static_cast<float*>(g.c[bi]) + (long)s * g.part_stride;
-    ML::epilogue(acc, [&](int r, int c, float v) {
-      const int gm = m0 + r, gn = n0 + c;
-      if (gm < g.M && gn < g.N) P[(long)gm * g.N + gn] = v;
-    });
-    return;
+  // ---- epilogue: stage each 64-row half of the fp32 tile in LDS, then every thread
+  // finishes 8 consecutive columns of a row and writes them with 16-byte stores.
+  const bool partial = g.splits > 1;
+  TO* C = partial ? nullptr : static_cast<TO*>(g.c[bi]);
+  float* P = partial ? static_cast<float*>(g.c[bi]) + (long)s * g.part_stride : nullptr;
+  const long ldc = partial ? (long)g.N : g.ldc;
+  const float* bias = partial ? nullptr : g.bias[bi];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, tid = threadIdx.x;
+  constexpr int CLD = BN + 4;
+  float* L = reinterpret_cast<float*>(lds);
+  const int cg = (tid & 15) * 8;
+  for (int hf = 0; hf < 2; ++hf) {
+    if ((wave >> 1) == hf) {
+      const int wn = (wave & 1) * (BN / 2);
+#pragma unroll
+      for (int i = 0; i < ML::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < ML::TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            L[(16 * i + 4 * (lane >> 4) + r) * CLD + wn + 16 * j + (lane & 15)] = acc[i][j][r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int rl = (tid >> 4) + 16 * k;
+      const int gm = m0 + hf * 64 + rl, gn = n0 + cg;
+      if (gm < g.M && gn < g.N) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = L[rl * CLD + cg + e];
+        const bool full = gn + 8 <= g.N && g.vec_ok;
+        if (partial) {
+          float* dst = P + (long)gm * ldc + gn;
+          if (full) st8(dst, v);
+          else
+            for (int e = 0; e < 8 && gn + e < g.N; ++e) dst[e] = v[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float x = v[e] * g.alpha;
+            if (bias && gn + e < g.N) x += bias[gn + e];
+            if (g.relu) x = fmaxf(x, 0.f);
+            if (g.drop_thresh) x *= tt_dropout_scale(g.drop_seed, gm, gn + e, g.drop_thresh, g.drop_inv_keep);
+            v[e] = x;
+          }
+          TO* dst = C + (long)gm * ldc + gn;
+          if (full) {
+            if (g.beta) {
+              float o[8];
+              ld8(dst, o);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] += o[e];
+            }
+            st8(dst, v);
+          } else {
+            for (int e = 0; e < 8 && gn + e < g.N; ++e) {
+              float x = v[e];
+              if (g.beta) x += Elt<TO>::ld(dst + e);
+              Elt<TO>::st(dst + e, x);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
   }
-  TO* C = static_cast<TO*>(g.c[bi]);
-  const float* bias = g.bias[bi];
-  ML::epilogue(acc, [&](int r, int c, float v) {
-    const int gm = m0 + r, gn = n0 + c;
-    if (gm >= g.M || gn >= g.N) return;
-    v *= g.alpha;
-    if (bias) v += bias[gn];
-    if (g.relu) v = fmaxf(v, 0.f);
-    if (g.drop_thresh) v *= tt_dropout_scale(g.drop_seed, gm, gn, g.drop_thresh, g.drop_inv_keep);
-    TO* p = C + (long)gm * g.ldc + gn;
-    if (g.beta) v += Elt<TO>::ld(p);
-    Elt<TO>::st(p, v);
-  });
 }
 
 // out_b[m][n] = alpha * sum_s part_b[s][m][n] (+ bias[n]) (+ out_b)
@@ -199,9 +246,16 @@ extern "C" int tt_gemm(int dtype, int out_dtype, int a_kouter, int b_kouter, int
   dim3 grid(tt_ceil_div(n, BN), tt_ceil_div(m, BM), nbatch * splits);
   TT_CHECK_ARG(grid.y <= 65535, "tt_gemm: m=%d too large", m);
 
+  {
+    const int osz = out_dtype == TT_DT_BF16 ? 2 : 4;
+    bool ok = (ldc * osz) % 16 == 0;
+    for (int b = 0; b < nbatch; ++b) ok = ok && ((uintptr_t)batch->c[b] % 16 == 0);
+    g.vec_ok = ok;
+  }
   if (splits > 1) {
     GemmArgs gp = g;
     gp.part_stride = (long)m * n;
+    gp.vec_ok = (n % 4 == 0);
     for (int b = 0; b < nbatch; ++b) gp.c[b] = splitk_ws + (long)b * splits * gp.part_stride;
     int rc = dtype == TT_DT_BF16 ? launch_gemm<bf16_t, float>(a_kouter, b_kouter, shift, gp, nbatch, grid, st)
                                  : launch_gemm<float, float>(a_kouter, b_kouter, shift, gp, nbatch, grid, st);

@@ -72,8 +72,11 @@ __global__ __launch_bounds__(256) void gru_fwd_step(FwdArgs a) {
     ML::run(la, lb, H, 0, nk, lds, acc);
   }
 
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wm = (wave >> 1) * 64, half = wave & 1;
+  // ---- epilogue, one 64-row half at a time: stage the fp32 gate tile in LDS, then
+  // every thread updates 8 consecutive hidden units of a row with 16-byte accesses.
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, tid = threadIdx.x;
+  float* L = reinterpret_cast<float*>(lds);  // [3][64][FLD]
+  constexpr int FLD = 68;                    // 64 units + 16 B pad
   const int cur = s & 1, prv = cur ^ 1;
   const T* G = static_cast<const T*>(R.g);
   T* Yw = static_cast<T*>(R.y);
@@ -81,42 +84,70 @@ __global__ __launch_bounds__(256) void gru_fwd_step(FwdArgs a) {
   T* S = static_cast<T*>(R.save);
   float* hs_cur = R.hs + (long)cur * a.B * H;
   const float* hs_prv = R.hs + (long)prv * a.B * H;
+  for (int hf = 0; hf < 2; ++hf) {
+    if ((wave >> 1) == hf) {
+      const int nb = (wave & 1) * 32;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+      for (int g = 0; g < 3; ++g)
 #pragma unroll
-    for (int jh = 0; jh < 2; ++jh)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int b = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
-        const int j = j0 + half * 32 + 16 * jh + (lane & 15);
-        if (b >= a.B || j >= H) continue;
+          for (int jh = 0; jh < 2; ++jh)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              L[(g * 64 + 16 * i + 4 * (lane >> 4) + r) * FLD + nb + 16 * jh + (lane & 15)] = acc[i][g * 2 + jh][r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int rl = (tid >> 3) + 32 * k, jg = (tid & 7) * 8;
+      const int b = m0 + hf * 64 + rl, j = j0 + jg;
+      if (b < a.B && j < H) {
         const long row = (long)b * T_ + t;
-        const T* gp = G + row * a.ldg + j;
-        const float xr = Elt<T>::ld(gp), xz = Elt<T>::ld(gp + H), xn = Elt<T>::ld(gp + 2 * H);
-        const float ghn = acc[i][4 + jh][r] + R.bhn[j];
-        const float ar = xr + acc[i][jh][r], az = xz + acc[i][2 + jh][r];
-        const float rg = tt_sigmoid(ar);
-        const float zg = tt_sigmoid(az);
-        const float an = xn + rg * ghn;
-        const float ng = tt_tanh(an);
-        const float hp = s > 0 ? hs_prv[(long)b * H + j] : 0.f;
-        const float hn = (1.f - zg) * ng + zg * hp;
-        hs_cur[(long)b * H + j] = hn;
-        Elt<T>::st(Yw + row * a.ldy + j, hn);
+        float xr[8], xz[8], xn[8], hp[8], bn[8], y[8], sr[8], sz[8], sn[8], sg[8];
+        ld8(G + row * a.ldg + j, xr);
+        ld8(G + row * a.ldg + H + j, xz);
+        ld8(G + row * a.ldg + 2 * H + j, xn);
+        ld8(R.bhn + j, bn);
+        if (s > 0) ld8(hs_prv + (long)b * H + j, hp);
+        else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) hp[e] = 0.f;
+        }
+        const float* Lr = L + (0 * 64 + rl) * FLD + jg;
+        const float* Lz = L + (1 * 64 + rl) * FLD + jg;
+        const float* Ln = L + (2 * 64 + rl) * FLD + jg;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float ghn = Ln[e] + bn[e];
+          const float ar = xr[e] + Lr[e], az = xz[e] + Lz[e];
+          const float rg = tt_sigmoid(ar), zg = tt_sigmoid(az);
+          const float an = xn[e] + rg * ghn;
+          const float ng = tt_tanh(an);
+          y[e] = (1.f - zg) * ng + zg * hp[e];
+          // pre-activations, not gate values: the backward recomputes sigma/tanh in
+          // fp32, so 1-z and 1-n^2 keep full precision even with bf16 storage
+          sr[e] = ar; sz[e] = az; sn[e] = an; sg[e] = ghn;
+        }
+        st8(hs_cur + (long)b * H + j, y);
+        st8(Yw + row * a.ldy + j, y);
         T* sp = S + row * (4L * H) + j;
-        // pre-activations, not gate values: the backward recomputes sigma/tanh in fp32,
-        // so 1-z and 1-n^2 keep full precision even with bf16 storage
-        Elt<T>::st(sp, ar);
-        Elt<T>::st(sp + H, az);
-        Elt<T>::st(sp + 2 * H, an);
-        Elt<T>::st(sp + 3 * H, ghn);
+        st8(sp, sr);
+        st8(sp + H, sz);
+        st8(sp + 2 * H, sn);
+        st8(sp + 3 * H, sg);
         if (X1) {
-          const float m = a.drop_thresh ? tt_dropout_scale(R.seed, (uint32_t)row, (uint32_t)(R.col0 + j),
-                                                           a.drop_thresh, a.inv_keep)
-                                        : 1.f;
-          Elt<T>::st(X1 + row * a.ldy + j, hn * m);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            y[e] *= a.drop_thresh ? tt_dropout_scale(R.seed, (uint32_t)row, (uint32_t)(R.col0 + j + e),
+                                                     a.drop_thresh, a.inv_keep)
+                                  : 1.f;
+          st8(X1 + row * a.ldy + j, y);
         }
       }
+    }
+    __syncthreads();
+  }
 }
 
 template <typename T>
@@ -145,79 +176,125 @@ __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
     ML::run(la, lb, K, 0, nk, lds, acc);
   }
 
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  // ---- epilogue, one 64-row half at a time through LDS; each thread owns 8
+  // consecutive units of a row (16-byte accesses) for 4 rows per half.
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, tid = threadIdx.x;
+  float* L = reinterpret_cast<float*>(lds);  // [64][BLD]
+  constexpr int BLD = 132;                   // 128 units + 16 B pad
   const int cur = s & 1, nxt = cur ^ 1;
   const T* S = static_cast<const T*>(R.save);
   const T* Y = static_cast<const T*>(R.y);
   const T* DY = static_cast<const T*>(R.dy);
   T* DGX = static_cast<T*>(R.dgx);
   T* DGHw = static_cast<T*>(R.dgh);
-  float* dh_cur = R.dh + (long)cur * a.B * H;
-  const float* dh_nxt = R.dh + (long)nxt * a.B * H;
+  float* cr_cur = R.dh + (long)cur * a.B * H;        // carry_s = dh_s * z_s
+  const float* cr_nxt = R.dh + (long)nxt * a.B * H;  // carry_{s+1}
   const long S4 = 4L * H;
-
+  const int jg = (tid & 15) * 8;
+  const int j = j0 + jg;
+  float bsum[4][8];
 #pragma unroll
-  for (int jt = 0; jt < 4; ++jt) {
-    const int j = j0 + wn + 16 * jt + (lane & 15);
-    float sr = 0.f, sz = 0.f, sn = 0.f, shn = 0.f;
+  for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int e = 0; e < 8; ++e) bsum[q][e] = 0.f;
+  for (int hf = 0; hf < 2; ++hf) {
+    if ((wave >> 1) == hf) {
+      const int wn = (wave & 1) * 64;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int b = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
-        if (b >= a.B || j >= H) continue;
-        const long row = (long)b * T_ + t;
-        float carry;
-        if (!last) {
-          carry = dh_nxt[(long)b * H + j] * tt_sigmoid(Elt<T>::ld(S + ((long)b * T_ + tn) * S4 + H + j));
-        } else {
-          carry = R.dfinal ? R.dfinal[(long)b * a.ldf + j] : 0.f;
-        }
-        float dht = acc[i][jt][r] + carry;
-        if (DY) dht += Elt<T>::ld(DY + row * a.ldy + j);
-        const T* sp = S + row * S4 + j;
-        const float ar = Elt<T>::ld(sp), az = Elt<T>::ld(sp + H), an = Elt<T>::ld(sp + 2 * H),
-                    ghn = Elt<T>::ld(sp + 3 * H);
-        const float rg = tt_sigmoid(ar), omr = tt_sigmoid(-ar);
-        const float zg = tt_sigmoid(az), omz = tt_sigmoid(-az);
-        const float ng = tt_tanh(an);
-        const float hp = s > 0 ? Elt<T>::ld(Y + ((long)b * T_ + tp) * a.ldy + j) : 0.f;
-        const float dn = dht * omz;
-        const float dz = dht * (hp - ng);
-        const float dnp = dn * tt_sech2(an);
-        const float drp = dnp * ghn * rg * omr;
-        const float dzp = dz * zg * omz;
-        const float dhn = dnp * rg;
-        dh_cur[(long)b * H + j] = dht;
-        T* gx = DGX + row * a.ldd + j;
-        T* gh = DGHw + row * a.ldd + j;
-        Elt<T>::st(gx, drp);
-        Elt<T>::st(gx + H, dzp);
-        Elt<T>::st(gx + 2 * H, dnp);
-        Elt<T>::st(gh, drp);
-        Elt<T>::st(gh + H, dzp);
-        Elt<T>::st(gh + 2 * H, dhn);
-        sr += drp; sz += dzp; sn += dnp; shn += dhn;
-      }
-    // bias partial sums: reduce the 4 row groups sharing this column
-    sr += __shfl_xor(sr, 16, 64); sr += __shfl_xor(sr, 32, 64);
-    sz += __shfl_xor(sz, 16, 64); sz += __shfl_xor(sz, 32, 64);
-    sn += __shfl_xor(sn, 16, 64); sn += __shfl_xor(sn, 32, 64);
-    shn += __shfl_xor(shn, 16, 64); shn += __shfl_xor(shn, 32, 64);
-    if (lane < 16 && j < H) {
-      float* pb = R.dbias + (long)(blockIdx.y * 2 + (wave >> 1)) * (4L * H) + j;
-      pb[0] += sr;
-      pb[H] += sz;
-      pb[2 * H] += sn;
-      pb[3 * H] += shn;
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            L[(16 * i + 4 * (lane >> 4) + r) * BLD + wn + 16 * jt + (lane & 15)] = acc[i][jt][r];
     }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int rl = (tid >> 4) + 16 * k;
+      const int b = m0 + hf * 64 + rl;
+      if (b < a.B && j < H) {
+        const long row = (long)b * T_ + t;
+        float cin[8], dy[8], ar[8], az[8], an[8], gh[8], hp[8];
+        if (!last) ld8(cr_nxt + (long)b * H + j, cin);
+        else if (R.dfinal) ld8(R.dfinal + (long)b * a.ldf + j, cin);
+        else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cin[e] = 0.f;
+        }
+        if (DY) ld8(DY + row * a.ldy + j, dy);
+        else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dy[e] = 0.f;
+        }
+        const T* sp = S + row * S4 + j;
+        ld8(sp, ar);
+        ld8(sp + H, az);
+        ld8(sp + 2 * H, an);
+        ld8(sp + 3 * H, gh);
+        if (s > 0) ld8(Y + ((long)b * T_ + tp) * a.ldy + j, hp);
+        else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) hp[e] = 0.f;
+        }
+        const float* Lc = L + rl * BLD + jg;
+        float o_r[8], o_z[8], o_n[8], o_hn[8], cout[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float dht = Lc[e] + cin[e] + dy[e];
+          const float rg = tt_sigmoid(ar[e]), omr = tt_sigmoid(-ar[e]);
+          const float zg = tt_sigmoid(az[e]), omz = tt_sigmoid(-az[e]);
+          const float ng = tt_tanh(an[e]);
+          const float dnp = dht * omz * tt_sech2(an[e]);
+          const float drp = dnp * gh[e] * rg * omr;
+          const float dzp = dht * (hp[e] - ng) * zg * omz;
+          o_r[e] = drp; o_z[e] = dzp; o_n[e] = dnp; o_hn[e] = dnp * rg;
+          cout[e] = dht * zg;
+          bsum[0][e] += drp; bsum[1][e] += dzp; bsum[2][e] += dnp; bsum[3][e] += dnp * rg;
+        }
+        st8(cr_cur + (long)b * H + j, cout);
+        T* gx = DGX + row * a.ldd + j;
+        T* gw = DGHw + row * a.ldd + j;
+        st8(gx, o_r);
+        st8(gx + H, o_z);
+        st8(gx + 2 * H, o_n);
+        st8(gw, o_r);
+        st8(gw + H, o_z);
+        st8(gw + 2 * H, o_hn);
+      }
+    }
+    __syncthreads();
+  }
+  // bias partial sums of this 128-row tile: lanes l, l^16, l^32, l^48 share columns
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = bsum[q][e];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      bsum[q][e] = v;
+    }
+  float* red = L;  // [4 waves][4][128]
+  if (lane < 16) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[(wave * 4 + q) * 128 + lane * 8 + e] = bsum[q][e];
+  }
+  __syncthreads();
+  if (tid < 128 && j0 + tid < H) {
+    float* pb = R.dbias + (long)blockIdx.y * (4L * H) + j0 + tid;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      pb[q * H] += red[(0 * 4 + q) * 128 + tid] + red[(1 * 4 + q) * 128 + tid] + red[(2 * 4 + q) * 128 + tid] +
+                   red[(3 * 4 + q) * 128 + tid];
   }
 }
 
 }  // namespace
 
-extern "C" int tt_gru_bias_rows(int B) { return tt_ceil_div(B, 128) * 2; }
+extern "C" int tt_gru_bias_rows(int B) { return tt_ceil_div(B, 128); }
 
 extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B, int T, int H, long ldg,
                           long ldy, float drop_p, void* stream) {

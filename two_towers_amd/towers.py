@@ -27,6 +27,7 @@ from ._lib import GruBwdRec, GruFwdRec, HeadBwdIO, HeadFwdIO, call, dtype_code, 
 
 PARAMS_PER_TOWER = 22
 LN_EPS = 1e-5
+HEAD_DT = torch.float32
 
 
 def gru_param_names():
@@ -76,11 +77,14 @@ class _Packed:
             self.bias.append(torch.cat(bs).float().contiguous())
             self.whh.append([g[f"weight_hh_l{layer}{s}"].to(dt).contiguous() for s in ("", "_reverse")])
             self.bhn.append([g[f"bias_hh_l{layer}{s}"][2 * H:].float().contiguous() for s in ("", "_reverse")])
-        self.w1 = hd["0.weight"].to(dt).contiguous()
+        # The projection head always runs in fp32 (HEAD_DT): it is <1% of the FLOPs, and its
+        # backward is where the batch-wide cancellation of the contrastive-loss gradient
+        # would otherwise lose most of its precision to a bf16 cast.
+        self.w1 = hd["0.weight"].float().contiguous()
         self.b1 = hd["0.bias"].float().contiguous()
         self.ln_g = hd["1.weight"].float().contiguous()
         self.ln_b = hd["1.bias"].float().contiguous()
-        self.w2 = hd["3.weight"].to(dt).contiguous()
+        self.w2 = hd["3.weight"].float().contiguous()
         self.b2 = hd["3.bias"].float().contiguous()
 
 
@@ -232,13 +236,13 @@ class TowersFn(torch.autograd.Function):
         hcat = []
         for ti in range(n):
             y = Y1[ti].view(B, T, 2 * H)
-            hcat.append(torch.cat([y[:, T - 1, :H], y[:, 0, H:]], 1).contiguous())
+            hcat.append(torch.cat([y[:, T - 1, :H], y[:, 0, H:]], 1).to(HEAD_DT).contiguous())
         outs, p1s, means, rstds, us = [], [], [], [], []
         io = (HeadFwdIO * n)()
         for ti in range(n):
             pk = packs[ti]
-            p1 = _alloc((B, 2 * h), dt, dev)
-            u = _alloc((B, 2 * h), dt, dev)
+            p1 = _alloc((B, 2 * h), HEAD_DT, dev)
+            u = _alloc((B, 2 * h), HEAD_DT, dev)
             mean = _alloc((B,), torch.float32, dev)
             rstd = _alloc((B,), torch.float32, dev)
             out = _alloc((B, h), torch.float32, dev)
@@ -248,7 +252,7 @@ class TowersFn(torch.autograd.Function):
             q.x, q.p1, q.mean, q.rstd, q.u, q.out = (hcat[ti].data_ptr(), p1.data_ptr(), mean.data_ptr(),
                                                      rstd.data_ptr(), u.data_ptr(), out.data_ptr())
             outs.append(out); p1s.append(p1); means.append(mean); rstds.append(rstd); us.append(u)
-        call("tt_proj_head_fwd", dtype_code(dt), io, n, B, h, LN_EPS, stream_ptr(dev))
+        call("tt_proj_head_fwd", dtype_code(HEAD_DT), io, n, B, h, LN_EPS, stream_ptr(dev))
         ctx.cfg = cfg
         ctx.dims = (B, T, Ep)
         ctx.seeds = seeds
@@ -269,7 +273,7 @@ class TowersFn(torch.autograd.Function):
         # ---- projection head
         head_grads = []
         dhcat = []
-        ws = _alloc((lib.tt_proj_head_bwd_ws_size(dtype_code(dt), B, h),), torch.uint8, dev)
+        ws = _alloc((lib.tt_proj_head_bwd_ws_size(dtype_code(HEAD_DT), B, h),), torch.uint8, dev)
         for ti in range(n):
             g = gouts[ti]
             g = torch.zeros(B, h, dtype=torch.float32, device=dev) if g is None else g.float().contiguous()
@@ -289,7 +293,7 @@ class TowersFn(torch.autograd.Function):
             io.dw1, io.db1, io.dg, io.dbeta, io.dw2, io.db2 = (dw1.data_ptr(), db1.data_ptr(), dg.data_ptr(),
                                                                dbeta.data_ptr(), dw2.data_ptr(), db2.data_ptr())
             io.ws = ws.data_ptr()
-            call("tt_proj_head_bwd", dtype_code(dt), ctypes.byref(io), 1, B, h, LN_EPS, st)
+            call("tt_proj_head_bwd", dtype_code(HEAD_DT), ctypes.byref(io), 1, B, h, LN_EPS, st)
             head_grads.append([dw1, db1, dg, dbeta, dw2, db2])
             dhcat.append(dx)
         # ---- GRU layer 1: dfinal enters at the last processed step of each direction

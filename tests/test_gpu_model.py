@@ -44,12 +44,20 @@ def test_forward_backward_fp32(E, h, B, T):
 
 
 def test_forward_backward_bf16():
+    """bf16 storage / fp32 accumulation vs the fp32 oracle run on the same bf16-rounded
+    inputs and weights (so only the kernels' internal rounding is compared).
+    Tolerances: loss 1e-3 relative; per-parameter gradient cos >= 0.998 and
+    ||g - g_ref|| <= 6% ||g_ref||."""
     E, h, B, T = 64, 32, 96, 10
-    m, p = make_model(E, h, 1)
+    m, _ = make_model(E, h, 1)
+    with torch.no_grad():
+        for prm in m.parameters():
+            prm.copy_(prm.to(torch.bfloat16).float())
+    p = {k: v.detach().clone() for k, v in m.state_dict().items()}
     m = m.to(DEV).eval().set_compute_dtype(torch.bfloat16)
     g = torch.Generator().manual_seed(6)
-    q = torch.randn(B, T, E, generator=g)
-    d = torch.randn(B, T, E, generator=g)
+    q = torch.randn(B, T, E, generator=g).to(torch.bfloat16).float()
+    d = torch.randn(B, T, E, generator=g).to(torch.bfloat16).float()
     qv, dv = m(q.to(DEV), d.to(DEV))
     loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
     loss.backward()
@@ -58,15 +66,13 @@ def test_forward_backward_bf16():
     rl = cpu_ref.infonce(rq, rd)
     rl.backward()
     assert rel(qv, rq) < 3e-2 and rel(dv, rd) < 3e-2
-    assert abs(float(loss) - float(rl)) < 2e-2 * abs(float(rl))
-    # bf16 storage of activations and of the GRU's gate gradients: per-parameter
-    # gradient direction within cos >= 0.995 and norm error <= 10% of the fp32 oracle
+    assert abs(float(loss) - float(rl)) < 1e-3 * abs(float(rl))
     named = dict(m.named_parameters())
     for k in pr:
         a, b = named[k].grad.double().cpu(), pr[k].grad.double()
         cos = float((a * b).sum() / (a.norm() * b.norm()))
         frob = float((a - b).norm() / b.norm())
-        assert cos >= 0.995 and frob <= 0.10, (k, cos, frob)
+        assert cos >= 0.998 and frob <= 0.06, (k, cos, frob)
 
 
 def test_dropout_matches_counter_mask():

@@ -1,6 +1,9 @@
 // Generic batched MFMA GEMM (NT / NN / TN, optional split-K) and the C-ABI
 // entry points tt_gemm / tt_gemm_ws_size / tt_gemm_pick_splits.
 #include <stdarg.h>
+#include <stdlib.h>
+
+#include <type_traits>
 
 #include "tt_api.h"
 #include "tt_gemm_core.h"
@@ -35,17 +38,33 @@ struct GemmArgs {
   float drop_inv_keep;
   long part_stride;  // elements between split partials (fp32), 0 if no split
   int vec_ok;        // C rows 16-byte aligned: 8-column vector stores allowed
+  int force_regstage;
 };
 
 constexpr int BM = 128, BN = 128;
 
-template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO>
+// XCD-aware tile order: consecutive workgroup ids are dealt round-robin over the 8
+// XCDs, so remap them (bijectively) to give every XCD a contiguous run of tiles in
+// row-major order; the tiles of one A panel then share that XCD's L2.
+__device__ __forceinline__ void tile_of(int& mt, int& nt) {
+  const int ntn = gridDim.x, nwg = gridDim.x * gridDim.y;
+  const int bid = blockIdx.y * ntn + blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  mt = id / ntn;
+  nt = id - mt * ntn;
+}
+
+template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO, bool DMA>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
-  using ML = ttg::MainLoop<T, AKO, BKO, BM, BN>;
+  using ML = std::conditional_t<DMA, ttg::MainLoopDMA<T, AKO, BKO, BM, BN>, ttg::MainLoop<T, AKO, BKO, BM, BN>>;
   __shared__ __attribute__((aligned(16))) char lds[ML::LDS_BYTES];
   const int z = blockIdx.z;
   const int bi = z / g.splits, s = z % g.splits;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  int mt, nt;
+  tile_of(mt, nt);
+  const int m0 = mt * BM, n0 = nt * BN;
   const T* A = static_cast<const T*>(g.a[bi]);
   const T* B = static_cast<const T*>(g.b[bi]);
 
@@ -170,8 +189,16 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* ws, lon
 template <typename T, typename TO>
 int launch_gemm(int akout, int bkout, bool shift, const GemmArgs& g, int nbatch, dim3 grid,
                 hipStream_t st) {
-#define TT_L(AK, BK, SH) \
-  hipLaunchKernelGGL((gemm_kernel<T, AK, BK, SH, TO>), grid, dim3(256), 0, st, g)
+  // LDS-DMA staging needs whole 16-byte chunks along K (K-contig) or along the
+  // columns (K-outer); otherwise the register-staged loop masks element-wise.
+  constexpr int EPC = 16 / (int)sizeof(T);
+  const bool dma = (akout ? g.M % EPC == 0 : g.K % EPC == 0) && (bkout ? g.N % EPC == 0 : g.K % EPC == 0) &&
+                   !g.force_regstage;
+#define TT_L(AK, BK, SH)                                                                     \
+  do {                                                                                       \
+    if (dma) hipLaunchKernelGGL((gemm_kernel<T, AK, BK, SH, TO, true>), grid, dim3(256), 0, st, g);  \
+    else hipLaunchKernelGGL((gemm_kernel<T, AK, BK, SH, TO, false>), grid, dim3(256), 0, st, g);     \
+  } while (0)
   if (!akout && !bkout) TT_L(false, false, false);
   else if (!akout && bkout && !shift) TT_L(false, true, false);
   else if (!akout && bkout && shift) TT_L(false, true, true);
@@ -234,6 +261,8 @@ extern "C" int tt_gemm(int dtype, int out_dtype, int a_kouter, int b_kouter, int
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = m; g.N = n; g.K = k;
   g.alpha = alpha; g.beta = beta_accum; g.relu = relu; g.seq_t = seq_t;
+  static const int force_reg = getenv("TT_GEMM_REGSTAGE") ? atoi(getenv("TT_GEMM_REGSTAGE")) : 0;
+  g.force_regstage = force_reg;
   g.drop_seed = drop_seed;
   g.drop_thresh = drop_p > 0.f ? (uint32_t)(drop_p * 16777216.0f + 0.5f) : 0u;
   g.drop_inv_keep = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;

@@ -230,6 +230,96 @@ struct MainLoop {
   }
 };
 
+// ---- LDS-DMA main loop ----------------------------------------------------------
+// Same tile, images and fragment reads as MainLoop, but operands are staged with
+// global_load_lds_dwordx4: each wave-instruction writes 1 KiB of LDS linearly
+// (lane L -> base + 16 L), so the XOR swizzle is applied to the per-lane SOURCE
+// address instead of the LDS destination. Out-of-range chunks read a zero page.
+// Requires every 16-byte chunk to be entirely valid or entirely out of range:
+// K * sizeof(T) % 16 == 0 for K-contig operands, ncols % (16/sizeof(T)) == 0 for
+// K-outer ones. Double-buffered: the DMA of tile k+1 overlaps the MFMAs of tile k.
+__device__ __attribute__((weak)) uint4 g_tt_zero_page[64];
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <typename T, bool KO, int ROWS, class L>
+TT_DEV void stage_dma(const L& ld, int kt, int K, char* img) {
+  constexpr int CHUNKS = Img<T, KO, ROWS>::CHUNKS;
+  constexpr int EPC = Elt<T>::EPC;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = wave; i < CHUNKS / 64; i += 4) {
+    const int p = i * 64 + lane;  // image position of this lane's 16 bytes
+    const void* src = g_tt_zero_page;
+    if constexpr (!KO) {
+      const int row = p >> 3;
+      const int c = (p & 7) ^ ((row >> 1) & 7);
+      const T* rp = ld.rowptr(row);
+      const int k = kt * (KTB / (int)sizeof(T)) + c * EPC;
+      if (rp != nullptr && k < K) src = rp + k;
+    } else {
+      constexpr int CPR = ROWS * (int)sizeof(T) / 16;
+      const int kl = p / CPR, q = p % CPR;
+      int c;
+      if constexpr (sizeof(T) == 2) c = q ^ (ko_v(kl) << 1);
+      else c = q ^ (((kl >> 2) & 1) << 2);
+      const int k = kt * (KTB / (int)sizeof(T)) + kl;
+      const T* kp = (k < K) ? ld.kptr(k) : nullptr;
+      if (kp != nullptr && c * EPC < ld.ncols) src = kp + c * EPC;
+    }
+    __builtin_amdgcn_global_load_lds(src, (lds_void*)(img + i * 1024), 16, 0, 0);
+  }
+}
+
+template <typename T, bool AKO, bool BKO, int BM, int BN>
+struct MainLoopDMA {
+  using Base = MainLoop<T, AKO, BKO, BM, BN>;
+  using IA = typename Base::IA;
+  using IB = typename Base::IB;
+  static constexpr int STAGE = Base::STAGE;
+  static constexpr int LDS_BYTES = Base::LDS_BYTES;
+  static constexpr int TM = Base::TM, TN = Base::TN;
+
+  template <class LA, class LB>
+  TT_DEV static void run(const LA& la, const LB& lb, int K, int kt0, int kt1, char* lds, f32x4 (&acc)[TM][TN]) {
+    if (kt0 >= kt1) return;
+    const int wave = threadIdx.x >> 6;
+    const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
+    stage_dma<T, AKO, BM>(la, kt0, K, lds);
+    stage_dma<T, BKO, BN>(lb, kt0, K, lds + IA::BYTES);
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int cur = (kt - kt0) & 1;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile kt landed
+      __builtin_amdgcn_s_barrier();                      // ...and every wave's; stage cur^1 is free
+      const char* ia = lds + cur * STAGE;
+      const char* ib = ia + IA::BYTES;
+      // All of tile kt's fragments are read BEFORE the next DMA is issued: hipcc cannot
+      // tell the two stages apart and would otherwise wait for that DMA (vmcnt(0))
+      // ahead of the first ds_read, serialising the copy and the MFMAs.
+      uint4 fa[2][TM], fb[2][TN];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[ks][i] = frag<T, AKO>(ia, wm + 16 * i, ks);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[ks][j] = frag<T, BKO>(ib, wn + 16 * j, ks);
+      }
+      if (kt + 1 < kt1) {
+        char* nx = lds + (cur ^ 1) * STAGE;
+        stage_dma<T, AKO, BM>(la, kt + 1, K, nx);
+        stage_dma<T, BKO, BN>(lb, kt + 1, K, nx + IA::BYTES);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mma<T>(fa[ks][i], fb[ks][j], acc[i][j]);
+    }
+    __builtin_amdgcn_s_barrier();  // every wave done reading before the caller reuses LDS
+  }
+};
+
 // ---- common loaders ------------------------------------------------------------
 template <typename T>
 struct KCPlain {  // rows [r0, r0+ROWS) of a row-major [rows][ld] matrix

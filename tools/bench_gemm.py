@@ -1,0 +1,51 @@
+"""Micro-benchmark of tt_gemm on the step's GEMM shapes (HIP-event timed)."""
+import argparse
+import json
+import sys
+
+import torch
+
+import os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from two_towers_amd import ops  # noqa: E402
+
+SHAPES = {  # name: (m, n, k, a_kouter, b_kouter, nbatch, out_bf16)
+    "input_proj_l1": (524288, 3072, 1024, 0, 0, 2, 1),
+    "input_proj_l0": (524288, 3072, 304, 0, 0, 2, 1),
+    "dgrad_l1": (524288, 1024, 3072, 0, 1, 1, 1),
+    "wgrad_ih1": (1536, 1024, 524288, 1, 1, 4, 0),
+    "wgrad_hh": (1536, 512, 524288, 1, 1, 4, 0),
+    "square8k": (8192, 8192, 8192, 0, 0, 1, 1),
+}
+
+
+def run(name, iters):
+    m, n, k, ak, bk, nb, obf = SHAPES[name]
+    dt = torch.bfloat16
+    A = [torch.randn((k, m) if ak else (m, k), device="cuda").to(dt) for _ in range(nb)]
+    B = [torch.randn((k, n) if bk else (n, k), device="cuda").to(dt) for _ in range(nb)]
+    odt = dt if obf else torch.float32
+    C = [torch.empty(m, n, device="cuda", dtype=odt) for _ in range(nb)]
+    bias = [torch.randn(n, device="cuda") for _ in range(nb)] if obf else None
+    f = lambda: ops.gemm(A, B, C, m=m, n=n, k=k, lda=m if ak else k, ldb=n if bk else k, ldc=n, a_kouter=bool(ak),
+                         b_kouter=bool(bk), dtype=dt, out_dtype=odt, bias=bias)
+    f()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        f()
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / iters
+    tf = 2.0 * m * n * k * nb / (ms * 1e-3) / 1e12
+    return {"shape": name, "ms": round(ms, 3), "tflops": round(tf, 1)}
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", default=",".join(SHAPES))
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    for nm in a.shapes.split(","):
+        print(json.dumps(run(nm, a.iters)), flush=True)

@@ -61,6 +61,29 @@ TT_DEV void st8(bf16_t* p, const float (&f)[8]) {
   *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// Streaming stores: buffer_store_dwordx4 ... sc1 writes through and DROPS the line from
+// the XCD's L2 (MI355X_MICROARCH.md, store flavours), so multi-GB output streams do not
+// evict the operands that the other workgroups of the XCD are still re-reading.
+// The descriptor base must be wave-uniform; byte offsets are per lane (< 2 GiB).
+typedef unsigned tt_u32x4 __attribute__((vector_size(16)));
+TT_DEV __amdgpu_buffer_rsrc_t tt_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+TT_DEV void st16_sc1(__amdgpu_buffer_rsrc_t r, int off, uint4 v) {
+  tt_u32x4 w = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 16);
+}
+TT_DEV void st8_sc1(__amdgpu_buffer_rsrc_t r, int off, const float (&f)[8], float*) {
+  st16_sc1(r, off, make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3])));
+  st16_sc1(r, off + 16, make_uint4(__float_as_uint(f[4]), __float_as_uint(f[5]), __float_as_uint(f[6]), __float_as_uint(f[7])));
+}
+TT_DEV void st8_sc1(__amdgpu_buffer_rsrc_t r, int off, const float (&f)[8], bf16_t*) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+  st16_sc1(r, off, make_uint4(w[0], w[1], w[2], w[3]));
+}
+
 TT_DEV float tt_sigmoid(float x) { return 1.0f / (1.0f + __expf(-x)); }
 TT_DEV float tt_tanh(float x) {
   // tanh(x) = 1 - 2/(exp(2x)+1); saturates cleanly for large |x|.

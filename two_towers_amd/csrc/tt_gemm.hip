@@ -39,32 +39,36 @@ struct GemmArgs {
   long part_stride;  // elements between split partials (fp32), 0 if no split
   int vec_ok;        // C rows 16-byte aligned: 8-column vector stores allowed
   int force_regstage;
+  int bias_vec_ok;  // every bias pointer 16-byte aligned
+  int stream_out;   // write-through (sc1) output stores: big outputs
 };
 
-constexpr int BM = 128, BN = 128;
+constexpr int BM = 128, BN = 128;  // tile of the register-staged / small path
 
-// XCD-aware tile order: consecutive workgroup ids are dealt round-robin over the 8
-// XCDs, so remap them (bijectively) to give every XCD a contiguous run of tiles in
-// row-major order; the tiles of one A panel then share that XCD's L2.
-__device__ __forceinline__ void tile_of(int& mt, int& nt) {
-  const int ntn = gridDim.x, nwg = gridDim.x * gridDim.y;
-  const int bid = blockIdx.y * ntn + blockIdx.x;
+// XCD-aware order over a 1-D grid: consecutive workgroup ids are dealt round-robin
+// over the 8 XCDs, so remap them (bijectively) to give every XCD a contiguous run of
+// ids. Ids enumerate (batch*split, m-tile, n-tile) with the n-tile fastest, so the
+// tiles of one A panel, and all tiles of one split-K slice, share an XCD's L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int xcd = bid & 7, loc = bid >> 3;
   const int q = nwg >> 3, r = nwg & 7;
-  const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
-  mt = id / ntn;
-  nt = id - mt * ntn;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
-template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO, bool DMA>
-__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
-  using ML = std::conditional_t<DMA, ttg::MainLoopDMA<T, AKO, BKO, BM, BN>, ttg::MainLoop<T, AKO, BKO, BM, BN>>;
-  __shared__ __attribute__((aligned(16))) char lds[ML::LDS_BYTES];
-  const int z = blockIdx.z;
-  const int bi = z / g.splits, s = z % g.splits;
-  int mt, nt;
-  tile_of(mt, nt);
-  const int m0 = mt * BM, n0 = nt * BN;
+template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO, int TBM, int TBN, int WGM, int WGN, bool DMA>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_kernel(GemmArgs g) {
+  using ML = std::conditional_t<DMA, ttg::DLoop<T, AKO, BKO, TBM, TBN, WGM, WGN>,
+                                ttg::MainLoop<T, AKO, BKO, TBM, TBN>>;
+  static_assert(DMA || (TBM == 128 && TBN == 128 && WGM == 2 && WGN == 2), "register path is 128x128");
+  constexpr int NT = 64 * WGM * WGN;
+  constexpr int LDSB = ML::LDS_BYTES > 64 * (TBN + 4) * 4 ? ML::LDS_BYTES : 64 * (TBN + 4) * 4;
+  __shared__ __attribute__((aligned(16))) char lds[LDSB];
+  const int ntn = (g.N + TBN - 1) / TBN, ntm = (g.M + TBM - 1) / TBM;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int bs = id / (ntm * ntn), tile = id - bs * (ntm * ntn);
+  const int mt = tile / ntn, nt = tile - mt * ntn;
+  const int bi = bs / g.splits, s = bs - bi * g.splits;
+  const int m0 = mt * TBM, n0 = nt * TBN;
   const T* A = static_cast<const T*>(g.a[bi]);
   const T* B = static_cast<const T*>(g.b[bi]);
 
@@ -96,7 +100,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     run(ttg::KCPlain<T>{A, g.lda, m0, g.M});
   }
 
-  // ---- epilogue: stage each 64-row half of the fp32 tile in LDS, then every thread
+  // ---- epilogue: stage 64-row slices of the fp32 tile in LDS, then every thread
   // finishes 8 consecutive columns of a row and writes them with 16-byte stores.
   const bool partial = g.splits > 1;
   TO* C = partial ? nullptr : static_cast<TO*>(g.c[bi]);
@@ -104,24 +108,39 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   const long ldc = partial ? (long)g.N : g.ldc;
   const float* bias = partial ? nullptr : g.bias[bi];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, tid = threadIdx.x;
-  constexpr int CLD = BN + 4;
+  constexpr int WTM = TBM / WGM, WTN = TBN / WGN;
+  const int wm = wave / WGN * WTM, wn = wave % WGN * WTN;
+  constexpr int CLD = TBN + 4;
+  constexpr int TPR = TBN / 8;          // threads per row
+  constexpr int RPP = NT / TPR;         // rows per pass per sweep
   float* L = reinterpret_cast<float*>(lds);
-  const int cg = (tid & 15) * 8;
-  for (int hf = 0; hf < 2; ++hf) {
-    if ((wave >> 1) == hf) {
-      const int wn = (wave & 1) * (BN / 2);
+  const int cg = (tid % TPR) * 8;
+  const __amdgpu_buffer_rsrc_t crs = tt_rsrc(partial ? (const void*)P : (const void*)(C + (long)m0 * ldc + n0));
+  float bv[8];  // this thread's 8 bias values (its columns are fixed)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bv[e] = 0.f;
+  if (bias) {
+    if (n0 + cg + 8 <= g.N && g.bias_vec_ok) ld8(bias + n0 + cg, bv);
+    else
+      for (int e = 0; e < 8; ++e)
+        if (n0 + cg + e < g.N) bv[e] = bias[n0 + cg + e];
+  }
+  for (int hf = 0; hf < TBM / 64; ++hf) {
+    if (wm <= hf * 64 && hf * 64 < wm + WTM) {
+      const int i0 = (hf * 64 - wm) / 16;
 #pragma unroll
       for (int i = 0; i < ML::TM; ++i)
+        if (i >= i0 && i < i0 + 4)
 #pragma unroll
-        for (int j = 0; j < ML::TN; ++j)
+          for (int j = 0; j < ML::TN; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            L[(16 * i + 4 * (lane >> 4) + r) * CLD + wn + 16 * j + (lane & 15)] = acc[i][j][r];
+            for (int r = 0; r < 4; ++r)
+              L[(16 * (i - i0) + 4 * (lane >> 4) + r) * CLD + wn + 16 * j + (lane & 15)] = acc[i][j][r];
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int rl = (tid >> 4) + 16 * k;
+    for (int k = 0; k < 64 / RPP; ++k) {
+      const int rl = tid / TPR + RPP * k;
       const int gm = m0 + hf * 64 + rl, gn = n0 + cg;
       if (gm < g.M && gn < g.N) {
         float v[8];
@@ -136,8 +155,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
         } else {
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            float x = v[e] * g.alpha;
-            if (bias && gn + e < g.N) x += bias[gn + e];
+            float x = v[e] * g.alpha + bv[e];
             if (g.relu) x = fmaxf(x, 0.f);
             if (g.drop_thresh) x *= tt_dropout_scale(g.drop_seed, gm, gn + e, g.drop_thresh, g.drop_inv_keep);
             v[e] = x;
@@ -150,7 +168,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 #pragma unroll
               for (int e = 0; e < 8; ++e) v[e] += o[e];
             }
-            st8(dst, v);
+            if (g.stream_out)
+              st8_sc1(crs, (int)(((long)(gm - m0) * ldc + (gn - n0)) * (long)sizeof(TO)), v, (TO*)nullptr);
+            else
+              st8(dst, v);
           } else {
             for (int e = 0; e < 8 && gn + e < g.N; ++e) {
               float x = v[e];
@@ -186,19 +207,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* ws, lon
   }
 }
 
-template <typename T, typename TO>
-int launch_gemm(int akout, int bkout, bool shift, const GemmArgs& g, int nbatch, dim3 grid,
-                hipStream_t st) {
-  // LDS-DMA staging needs whole 16-byte chunks along K (K-contig) or along the
-  // columns (K-outer); otherwise the register-staged loop masks element-wise.
-  constexpr int EPC = 16 / (int)sizeof(T);
-  const bool dma = (akout ? g.M % EPC == 0 : g.K % EPC == 0) && (bkout ? g.N % EPC == 0 : g.K % EPC == 0) &&
-                   !g.force_regstage;
-#define TT_L(AK, BK, SH)                                                                     \
-  do {                                                                                       \
-    if (dma) hipLaunchKernelGGL((gemm_kernel<T, AK, BK, SH, TO, true>), grid, dim3(256), 0, st, g);  \
-    else hipLaunchKernelGGL((gemm_kernel<T, AK, BK, SH, TO, false>), grid, dim3(256), 0, st, g);     \
-  } while (0)
+template <typename T, typename TO, int TBM, int TBN, int WGM, int WGN, bool DMA>
+int launch_t(int akout, int bkout, bool shift, const GemmArgs& g, long nwg, hipStream_t st) {
+  dim3 grid((unsigned)nwg), blk(64 * WGM * WGN);
+#define TT_L(AK, BK, SH) \
+  hipLaunchKernelGGL((gemm_kernel<T, AK, BK, SH, TO, TBM, TBN, WGM, WGN, DMA>), grid, blk, 0, st, g)
   if (!akout && !bkout) TT_L(false, false, false);
   else if (!akout && bkout && !shift) TT_L(false, true, false);
   else if (!akout && bkout && shift) TT_L(false, true, true);
@@ -210,6 +223,23 @@ int launch_gemm(int akout, int bkout, bool shift, const GemmArgs& g, int nbatch,
   return 0;
 }
 
+// 256x256 tiles (8 waves) for problems with enough tiles to fill the chip, else
+// 128x128 (4 waves); register staging only when a chunk can straddle a boundary.
+inline bool use_big(int m, int n, long tiles256) { return m >= 256 && n >= 256 && tiles256 >= 256; }
+
+template <typename T, typename TO>
+int launch_gemm(int akout, int bkout, bool shift, GemmArgs& g, int nbatch, hipStream_t st) {
+  constexpr int EPC = 16 / (int)sizeof(T);
+  const bool dma = (akout ? g.M % EPC == 0 : g.K % EPC == 0) && (bkout ? g.N % EPC == 0 : g.K % EPC == 0) &&
+                   g.force_regstage != 1;
+  const long t256 = (long)tt_ceil_div(g.M, 256) * tt_ceil_div(g.N, 256) * nbatch * g.splits;
+  if (dma && g.force_regstage != 2 && use_big(g.M, g.N, t256))
+    return launch_t<T, TO, 256, 256, 2, 4, true>(akout, bkout, shift, g, t256, st);
+  const long t128 = (long)tt_ceil_div(g.M, 128) * tt_ceil_div(g.N, 128) * nbatch * g.splits;
+  if (dma) return launch_t<T, TO, 128, 128, 2, 2, true>(akout, bkout, shift, g, t128, st);
+  return launch_t<T, TO, 128, 128, 2, 2, false>(akout, bkout, shift, g, t128, st);
+}
+
 }  // namespace
 
 extern "C" long tt_gemm_ws_size(int m, int n, int nbatch, int splits) {
@@ -217,13 +247,22 @@ extern "C" long tt_gemm_ws_size(int m, int n, int nbatch, int splits) {
 }
 
 extern "C" int tt_gemm_pick_splits(int m, int n, int k, int nbatch) {
-  const long tiles = (long)tt_ceil_div(m, BM) * tt_ceil_div(n, BN) * nbatch;
-  if (tiles >= 512) return 1;
-  const int nk = tt_ceil_div(k, 64);
-  int s = (int)((1024 + tiles - 1) / tiles);
-  s = s > nk / 8 ? nk / 8 : s;  // keep >= 8 K-tiles per split
-  if (s > 64) s = 64;
-  return s < 1 ? 1 : s;
+  // Enough workgroups for >= 2-3 rounds over the 256 CUs, with the last round as
+  // full as possible; never fewer than 8 K-tiles (64 bf16) per split.
+  const bool big = m >= 256 && n >= 256;
+  const long tiles = big ? (long)tt_ceil_div(m, 256) * tt_ceil_div(n, 256) * nbatch
+                         : (long)tt_ceil_div(m, BM) * tt_ceil_div(n, BN) * nbatch;
+  const long target = big ? 512 : 1024;
+  if (tiles >= target) return 1;
+  const int smax = std::max(1, std::min(64, tt_ceil_div(k, 64) / 8));
+  int best = 1;
+  double best_eff = 0.0;
+  for (int s = (int)std::max<long>(1, target / tiles); s <= std::min<long>(smax, 3 * target / tiles + 1); ++s) {
+    const long w = tiles * s;
+    const double eff = (double)w / (256.0 * (double)tt_ceil_div(w, 256));
+    if (eff > best_eff + 1e-9) { best_eff = eff; best = s; }
+  }
+  return std::min(best, smax);
 }
 
 extern "C" int tt_gemm(int dtype, int out_dtype, int a_kouter, int b_kouter, int m, int n, int k,
@@ -268,26 +307,31 @@ extern "C" int tt_gemm(int dtype, int out_dtype, int a_kouter, int b_kouter, int
   g.drop_inv_keep = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
   const int nk = tt_ceil_div((long)k * esz, 128);
   if (splits > nk) splits = nk > 0 ? nk : 1;
-  g.kt_per_split = tt_ceil_div(nk, splits);
+  g.kt_per_split = nk > 0 ? tt_ceil_div(nk, splits) : 1;
   splits = nk > 0 ? tt_ceil_div(nk, g.kt_per_split) : 1;
   g.splits = splits;
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  dim3 grid(tt_ceil_div(n, BN), tt_ceil_div(m, BM), nbatch * splits);
-  TT_CHECK_ARG(grid.y <= 65535, "tt_gemm: m=%d too large", m);
-
   {
     const int osz = out_dtype == TT_DT_BF16 ? 2 : 4;
     bool ok = (ldc * osz) % 16 == 0;
     for (int b = 0; b < nbatch; ++b) ok = ok && ((uintptr_t)batch->c[b] % 16 == 0);
     g.vec_ok = ok;
+    bool bok = true;
+    for (int b = 0; b < nbatch; ++b) bok = bok && ((uintptr_t)batch->bias[b] % 16 == 0);
+    g.bias_vec_ok = bok;
+    // outputs far larger than the L2s are streamed past them (sc1); ld*rows must
+    // stay addressable by a 32-bit per-tile byte offset
+    g.stream_out = ok && (long)m * n * osz >= (64L << 20) && (long)256 * ldc * osz < (1L << 31);
   }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  TT_CHECK_ARG((long)tt_ceil_div(m, 128) * tt_ceil_div(n, 128) * nbatch * splits < (1L << 31), "tt_gemm: too many tiles");
+
   if (splits > 1) {
     GemmArgs gp = g;
     gp.part_stride = (long)m * n;
     gp.vec_ok = (n % 4 == 0);
     for (int b = 0; b < nbatch; ++b) gp.c[b] = splitk_ws + (long)b * splits * gp.part_stride;
-    int rc = dtype == TT_DT_BF16 ? launch_gemm<bf16_t, float>(a_kouter, b_kouter, shift, gp, nbatch, grid, st)
-                                 : launch_gemm<float, float>(a_kouter, b_kouter, shift, gp, nbatch, grid, st);
+    int rc = dtype == TT_DT_BF16 ? launch_gemm<bf16_t, float>(a_kouter, b_kouter, shift, gp, nbatch, st)
+                                 : launch_gemm<float, float>(a_kouter, b_kouter, shift, gp, nbatch, st);
     if (rc) return rc;
     const long total = (long)m * n;
     dim3 rg((unsigned)std::min<long>(tt_ceil_div(total, 256), 2048), nbatch);
@@ -299,8 +343,8 @@ extern "C" int tt_gemm(int dtype, int out_dtype, int a_kouter, int b_kouter, int
     return 0;
   }
   if (dtype == TT_DT_BF16) {
-    return out_dtype == TT_DT_BF16 ? launch_gemm<bf16_t, bf16_t>(a_kouter, b_kouter, shift, g, nbatch, grid, st)
-                                   : launch_gemm<bf16_t, float>(a_kouter, b_kouter, shift, g, nbatch, grid, st);
+    return out_dtype == TT_DT_BF16 ? launch_gemm<bf16_t, bf16_t>(a_kouter, b_kouter, shift, g, nbatch, st)
+                                   : launch_gemm<bf16_t, float>(a_kouter, b_kouter, shift, g, nbatch, st);
   }
-  return launch_gemm<float, float>(a_kouter, b_kouter, shift, g, nbatch, grid, st);
+  return launch_gemm<float, float>(a_kouter, b_kouter, shift, g, nbatch, st);
 }

@@ -320,6 +320,119 @@ struct MainLoopDMA {
   }
 };
 
+// ---- generic LDS-DMA loop (any wave grid; 256-wide tiles) ------------------------
+// One LDS-DMA of 16 bytes per lane into LDS byte address lds_addr + 16*lane, issued
+// from inline asm so that hipcc neither counts it nor waits for it: the loop below
+// places every s_waitcnt vmcnt itself (recipe: cdna_hip_programming.md §5.7).
+TT_DEV void dma16(const void* src, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds_addr)
+               : "memory");
+}
+TT_DEV uint32_t lds_addr_of(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+// Image of one K-tile of an operand with ROWS tile rows: K-contig = ROWS x 128 B rows;
+// K-outer = ROWS/128 sub-images of [KT k][128 columns] (16 KiB each).
+template <typename T, bool KO, int ROWS>
+struct Img2 {
+  static constexpr int KOSUB = (KTB / (int)sizeof(T)) * 128 * (int)sizeof(T);
+  static constexpr int BYTES = KO ? (ROWS / 128) * KOSUB : ROWS * KTB;
+  static constexpr int CHUNKS = BYTES / 16;
+  static_assert(!KO || ROWS % 128 == 0, "K-outer tiles are multiples of 128 columns");
+};
+
+template <typename T, bool KO, int ROWS, int NW, class L>
+TT_DEV void stage_dma2(const L& ld, int kt, int K, char* img) {
+  using I = Img2<T, KO, ROWS>;
+  constexpr int EPC = Elt<T>::EPC;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr_of(img));
+#pragma unroll
+  for (int i = wave; i < I::CHUNKS / 64; i += NW) {
+    const int p = i * 64 + lane;
+    const void* src = g_tt_zero_page;
+    if constexpr (!KO) {
+      const int row = p >> 3;
+      const int c = (p & 7) ^ ((row >> 1) & 7);
+      const T* rp = ld.rowptr(row);
+      const int k = kt * (KTB / (int)sizeof(T)) + c * EPC;
+      if (rp != nullptr && k < K) src = rp + k;
+    } else {
+      const int sub = p >> 10, pp = p & 1023;
+      constexpr int CPR = 128 * (int)sizeof(T) / 16;
+      const int kl = pp / CPR, q = pp % CPR;
+      int c;
+      if constexpr (sizeof(T) == 2) c = q ^ (ko_v(kl) << 1);
+      else c = q ^ (((kl >> 2) & 1) << 2);
+      const int col = sub * 128 + c * EPC;
+      const int k = kt * (KTB / (int)sizeof(T)) + kl;
+      const T* kp = (k < K) ? ld.kptr(k) : nullptr;
+      if (kp != nullptr && col < ld.ncols) src = kp + col;
+    }
+    dma16(src, base + (uint32_t)i * 1024u);
+  }
+}
+
+template <typename T, bool KO>
+TT_DEV uint4 frag2(const char* img, int r0, int ks) {
+  if constexpr (!KO) return frag<T, false>(img, r0, ks);
+  else return frag<T, true>(img + (r0 >> 7) * Img2<T, true, 128>::KOSUB, r0 & 127, ks);
+}
+
+template <typename T, bool AKO, bool BKO, int BM, int BN, int WGM, int WGN>
+struct DLoop {
+  static constexpr int NW = WGM * WGN;
+  static constexpr int NT = 64 * NW;
+  using IA = Img2<T, AKO, BM>;
+  using IB = Img2<T, BKO, BN>;
+  static constexpr int STAGE = IA::BYTES + IB::BYTES;
+  static constexpr int LDS_BYTES = 2 * STAGE;
+  static constexpr int WTM = BM / WGM, WTN = BN / WGN;  // wave tile
+  static constexpr int TM = WTM / 16, TN = WTN / 16;
+  static_assert(IA::CHUNKS % 64 == 0 && IB::CHUNKS % 64 == 0, "tile/wave mismatch");
+
+  TT_DEV static int wave_m0() { return (int)(threadIdx.x >> 6) / WGN * WTM; }
+  TT_DEV static int wave_n0() { return (int)(threadIdx.x >> 6) % WGN * WTN; }
+
+  // Accumulates K-tiles [kt0, kt1) into acc (caller zeroes it); ends with a barrier.
+  template <class LA, class LB>
+  TT_DEV static void run(const LA& la, const LB& lb, int K, int kt0, int kt1, char* lds, f32x4 (&acc)[TM][TN]) {
+    if (kt0 >= kt1) return;
+    const int wm = wave_m0(), wn = wave_n0();
+    stage_dma2<T, AKO, BM, NW>(la, kt0, K, lds);
+    stage_dma2<T, BKO, BN, NW>(lb, kt0, K, lds + IA::BYTES);
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int cur = (kt - kt0) & 1;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile kt landed
+      __builtin_amdgcn_s_barrier();                      // every wave's; stage cur^1 is free
+      if (kt + 1 < kt1) {                                // tile kt+1 flies during tile kt's MFMAs
+        char* nx = lds + (cur ^ 1) * STAGE;
+        stage_dma2<T, AKO, BM, NW>(la, kt + 1, K, nx);
+        stage_dma2<T, BKO, BN, NW>(lb, kt + 1, K, nx + IA::BYTES);
+      }
+      const char* ia = lds + cur * STAGE;
+      const char* ib = ia + IA::BYTES;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        uint4 fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = frag2<T, AKO>(ia, wm + 16 * i, ks);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = frag2<T, BKO>(ib, wn + 16 * j, ks);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mma<T>(fa[i], fb[j], acc[i][j]);
+      }
+    }
+    __builtin_amdgcn_s_barrier();
+  }
+};
+
 // ---- common loaders ------------------------------------------------------------
 template <typename T>
 struct KCPlain {  // rows [r0, r0+ROWS) of a row-major [rows][ld] matrix

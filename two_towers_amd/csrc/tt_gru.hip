@@ -9,6 +9,8 @@
 // The forward tile is 128 batch rows x (3 gates x 64 hidden units): the B-tile rows
 // are ordered [unit half][gate][32 units] so that every lane holds r, z and n for
 // the same (b, j) in registers and the update needs no data exchange.
+#include <algorithm>
+
 #include "tt_api.h"
 #include "tt_gemm_core.h"
 
@@ -51,7 +53,7 @@ struct GateRows {
 
 template <typename T>
 __global__ __launch_bounds__(256) void gru_fwd_step(FwdArgs a) {
-  using ML = ttg::MainLoop<T, false, false, 128, 192>;
+  using ML = ttg::DLoop<T, false, false, 128, 192, 2, 2>;
   __shared__ __attribute__((aligned(16))) char lds[ML::LDS_BYTES];
   const FwdRec R = a.r[blockIdx.z];
   const int H = a.H, T_ = a.T, s = a.s;
@@ -84,6 +86,8 @@ __global__ __launch_bounds__(256) void gru_fwd_step(FwdArgs a) {
   T* S = static_cast<T*>(R.save);
   float* hs_cur = R.hs + (long)cur * a.B * H;
   const float* hs_prv = R.hs + (long)prv * a.B * H;
+  const __amdgpu_buffer_rsrc_t srs = tt_rsrc(S + ((long)m0 * T_ + t) * (4L * H));
+  const __amdgpu_buffer_rsrc_t xrs = tt_rsrc(X1 ? X1 + ((long)m0 * T_ + t) * a.ldy : Yw);
   for (int hf = 0; hf < 2; ++hf) {
     if ((wave >> 1) == hf) {
       const int nb = (wave & 1) * 32;
@@ -131,18 +135,20 @@ __global__ __launch_bounds__(256) void gru_fwd_step(FwdArgs a) {
         }
         st8(hs_cur + (long)b * H + j, y);
         st8(Yw + row * a.ldy + j, y);
-        T* sp = S + row * (4L * H) + j;
-        st8(sp, sr);
-        st8(sp + H, sz);
-        st8(sp + 2 * H, sn);
-        st8(sp + 3 * H, sg);
+        // saved pre-activations and the dropout copy are only read by later kernels:
+        // stream them past L2 (sc1) so Whh and the h_{s-1} rows stay resident
+        const int so = (int)((((long)(b - m0) * T_) * 4L * H + j) * (long)sizeof(T));
+        st8_sc1(srs, so, sr, (T*)nullptr);
+        st8_sc1(srs, so + H * (int)sizeof(T), sz, (T*)nullptr);
+        st8_sc1(srs, so + 2 * H * (int)sizeof(T), sn, (T*)nullptr);
+        st8_sc1(srs, so + 3 * H * (int)sizeof(T), sg, (T*)nullptr);
         if (X1) {
 #pragma unroll
           for (int e = 0; e < 8; ++e)
             y[e] *= a.drop_thresh ? tt_dropout_scale(R.seed, (uint32_t)row, (uint32_t)(R.col0 + j + e),
                                                      a.drop_thresh, a.inv_keep)
                                   : 1.f;
-          st8(X1 + row * a.ldy + j, y);
+          st8_sc1(xrs, (int)((((long)(b - m0) * T_) * a.ldy + j) * (long)sizeof(T)), y, (T*)nullptr);
         }
       }
     }
@@ -152,7 +158,7 @@ __global__ __launch_bounds__(256) void gru_fwd_step(FwdArgs a) {
 
 template <typename T>
 __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
-  using ML = ttg::MainLoop<T, false, true, 128, 128>;
+  using ML = ttg::DLoop<T, false, true, 128, 128, 2, 2>;
   __shared__ __attribute__((aligned(16))) char lds[ML::LDS_BYTES];
   const BwdRec R = a.r[blockIdx.z];
   const int H = a.H, T_ = a.T, s = a.s;
@@ -192,6 +198,7 @@ __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
   const long S4 = 4L * H;
   const int jg = (tid & 15) * 8;
   const int j = j0 + jg;
+  const __amdgpu_buffer_rsrc_t grs = tt_rsrc(DGX + ((long)m0 * T_ + t) * a.ldd);
   float bsum[4][8];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
@@ -253,11 +260,12 @@ __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
           bsum[0][e] += drp; bsum[1][e] += dzp; bsum[2][e] += dnp; bsum[3][e] += dnp * rg;
         }
         st8(cr_cur + (long)b * H + j, cout);
-        T* gx = DGX + row * a.ldd + j;
         T* gw = DGHw + row * a.ldd + j;
-        st8(gx, o_r);
-        st8(gx + H, o_z);
-        st8(gx + 2 * H, o_n);
+        // dL/dg is next read by the weight-gradient GEMMs only: stream it past L2
+        const int go = (int)((((long)(b - m0) * T_) * a.ldd + j) * (long)sizeof(T));
+        st8_sc1(grs, go, o_r, (T*)nullptr);
+        st8_sc1(grs, go + H * (int)sizeof(T), o_z, (T*)nullptr);
+        st8_sc1(grs, go + 2 * H * (int)sizeof(T), o_n, (T*)nullptr);
         st8(gw, o_r);
         st8(gw + H, o_z);
         st8(gw + 2 * H, o_hn);
@@ -305,6 +313,7 @@ extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B
   TT_CHECK_ARG(H % (16 / esz) == 0 && (ldy * esz) % 16 == 0, "tt_gru_fwd: H=%d/ldy=%ld misaligned", H, ldy);
   TT_CHECK_ARG(drop_p >= 0.f && drop_p < 1.f, "tt_gru_fwd: drop_p");
   TT_CHECK_ARG(tt_ceil_div(B, 128) <= 65535, "tt_gru_fwd: B too large");
+  TT_CHECK_ARG(128L * T * std::max(4L * H, ldy) * esz < (1L << 31), "tt_gru_fwd: tile byte offsets exceed 2 GiB");
   FwdArgs a{};
   for (int i = 0; i < nrec; ++i) {
     const tt_gru_fwd_rec& r = recs[i];
@@ -332,6 +341,7 @@ extern "C" int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B
   TT_CHECK_ARG(B > 0 && T > 0 && H > 0, "tt_gru_bwd: bad shape");
   const int esz = dtype == TT_DT_BF16 ? 2 : 4;
   TT_CHECK_ARG(H % (16 / esz) == 0 && (ldd * esz) % 16 == 0, "tt_gru_bwd: H=%d/ldd=%ld misaligned", H, ldd);
+  TT_CHECK_ARG(128L * T * ldd * esz < (1L << 31), "tt_gru_bwd: tile byte offsets exceed 2 GiB");
   hipStream_t st = (hipStream_t)stream;
   BwdArgs a{};
   for (int i = 0; i < nrec; ++i) {

@@ -178,30 +178,38 @@ def main():
     pairs = B * world * args.steps
     value = pairs / elapsed
 
-    # Roofline of the dominant kernel (largest device time inside the timed region).
+    # Rooflines from live HIP-event timings. Every region carries its algorithmic FLOPs
+    # and algorithmic HBM bytes; the binding roofline is the one whose floor time
+    # (FLOPs / MFMA peak vs bytes / HBM peak) is larger. `roofline` = dominant kernel
+    # (largest device time per step).
     peak = BF16_PEAK_TFS if dt == torch.bfloat16 else FP32_PEAK_TFS
-    flop_regions = {k: v for k, v in kt.items() if k not in ("embed_gather",)}
-    dom = max(flop_regions, key=lambda k: flop_regions[k]["ms_total"])
-    r = kt[dom]
-    achieved = r["work"] / (r["ms_total"] * 1e-3) / 1e12
-    roofline = {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": None,
-                "work_per_launch": r["work_per_launch"], "ms_per_launch": round(r["ms_per_launch"], 5)}
-    extra = {}
-    if "embed_gather" in kt:
-        g = kt["embed_gather"]
-        gbs = g["work"] / (g["ms_total"] * 1e-3) / 1e9
-        extra["embed_gather"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                 "frac": round(gbs / HBM_PEAK_GBS, 4), "ms_per_launch": round(g["ms_per_launch"], 5)}
-    for name in ("hardneg_topk", "infonce_fwd"):
-        if name in kt:
-            g = kt[name]
-            tfs = g["work"] / (g["ms_total"] * 1e-3) / 1e12
-            extra[name] = {"bound": "mfma", "achieved": round(tfs, 2), "peak": peak, "unit": "TFLOP/s",
-                           "frac": round(tfs / peak, 4), "ms_per_launch": round(g["ms_per_launch"], 5)}
+
+    def roof(name):
+        r = kt[name]
+        sec = r["ms_total"] * 1e-3
+        if name == "embed_gather":
+            flop_floor, byte_floor = 0.0, r["bytes"] / (HBM_PEAK_GBS * 1e9)
+        else:
+            flop_floor, byte_floor = r["work"] / (peak * 1e12), r["bytes"] / (HBM_PEAK_GBS * 1e9)
+        if byte_floor >= flop_floor:
+            ach = r["bytes"] / sec / 1e9
+            out = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_launch": round(r["bytes_per_launch"])}
+        else:
+            ach = r["work"] / sec / 1e12
+            out = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+                   "frac": round(ach / peak, 4), "flops_per_launch": round(r["work_per_launch"])}
+        out["ms_per_launch"] = round(r["ms_per_launch"], 5)
+        out["launches_per_step"] = r["launches"] // max(args.steps, 1)
+        return out
+
+    dom = max(kt, key=lambda k: kt[k]["ms_total"])
+    roofline = {"kernel": dom, **roof(dom), "traffic": None}
+    extra = {k: roof(k) for k in kt if k != dom}
     step_ms = 1e3 * elapsed / args.steps
     kernels = {k: {"ms_per_step": round(v["ms_total"] / args.steps, 3),
-                   "tflops": round(v["work"] / (v["ms_total"] * 1e-3) / 1e12, 1) if k != "embed_gather" else None}
+                   "tflops": round(v["work"] / (v["ms_total"] * 1e-3) / 1e12, 1) if k != "embed_gather" else None,
+                   "gbs": round(v["bytes"] / (v["ms_total"] * 1e-3) / 1e9, 1)}
                for k, v in sorted(kt.items(), key=lambda kv: -kv[1]["ms_total"])}
     if args.timing and rank == 0:
         import sys

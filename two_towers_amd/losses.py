@@ -57,7 +57,8 @@ class _NormCE(torch.autograd.Function):
         row = torch.empty(B, dtype=torch.float32, device=q.device)
         lib = _lib.load()
         ws = torch.empty(lib.tt_infonce_fwd_ws_size(B, nd), dtype=torch.uint8, device=q.device)
-        with timing.region("infonce_fwd", 1, 2.0 * B * nd * q.shape[1]):
+        esz = 2 if dt == torch.bfloat16 else 4
+        with timing.region("infonce_fwd", 1, 2.0 * B * nd * q.shape[1], float(esz * (B + nd) * q.shape[1] + 8 * B)):
             call("tt_infonce_fwd", dtype_code(dt), qn.data_ptr(), B, dn.data_ptr(), nd, q.shape[1], inv_tau,
                  offdiag, rank * B, lse.data_ptr(), row.data_ptr(), ws.data_ptr(), stream_ptr(q.device))
         out = torch.empty((), dtype=torch.float32, device=q.device)
@@ -180,7 +181,8 @@ def mine_hard_negatives(query_vecs: torch.Tensor, doc_vecs: torch.Tensor, label_
         lib = _lib.load()
         ws = torch.empty(lib.tt_hardneg_ws_size(dtype_code(compute_dtype), B, nd), dtype=torch.uint8,
                          device=qn.device)
-        with timing.region("hardneg_topk", 1, 2.0 * B * nd * h):
+        esz = 2 if compute_dtype == torch.bfloat16 else 4
+        with timing.region("hardneg_topk", 1, 2.0 * B * nd * h, float(esz * (B + nd) * h + B * k * 4)):
             call("tt_hardneg_topk", dtype_code(compute_dtype), qn.data_ptr(), B, dn.data_ptr(), nd, h,
                  label_offset, k, idx.data_ptr(), ptr(val), ws.data_ptr(), stream_ptr(qn.device))
     return (idx, val) if return_values else idx

@@ -21,7 +21,9 @@ def reset():
 
 
 @contextmanager
-def region(name: str, launches: int, work: float):
+def region(name: str, launches: int, work: float, nbytes: float = 0.0):
+    """work = algorithmic FLOPs (or bytes for pure data movement), nbytes =
+    algorithmic HBM bytes of the region (inputs read once + outputs written once)."""
     if not enabled:
         yield
         return
@@ -30,7 +32,7 @@ def region(name: str, launches: int, work: float):
     s.record()
     yield
     e.record()
-    _records[name].append((s, e, launches, work))
+    _records[name].append((s, e, launches, work, nbytes))
 
 
 def summary():
@@ -38,9 +40,10 @@ def summary():
     torch.cuda.synchronize()
     out = {}
     for name, recs in _records.items():
-        ms = sum(s.elapsed_time(e) for s, e, _, _ in recs)
+        ms = sum(r[0].elapsed_time(r[1]) for r in recs)
         n = sum(r[2] for r in recs)
         w = sum(r[3] for r in recs)
-        out[name] = dict(ms_total=ms, launches=n, work=w, ms_per_launch=ms / max(n, 1),
-                         work_per_launch=w / max(n, 1), calls=len(recs))
+        b = sum(r[4] for r in recs)
+        out[name] = dict(ms_total=ms, launches=n, work=w, bytes=b, ms_per_launch=ms / max(n, 1),
+                         work_per_launch=w / max(n, 1), bytes_per_launch=b / max(n, 1), calls=len(recs))
     return out

@@ -107,7 +107,8 @@ def featurize(x: torch.Tensor, table: torch.Tensor | None, Ep: int, dt: torch.dt
         out = _alloc((ids.numel(), Ep), dt, x.device)
         esz = 2 if dt == torch.bfloat16 else 4
         # algorithmic bytes per row: id + the E real columns read and written
-        with timing.region("embed_gather", 1, ids.numel() * (4 + 2 * table_cols(table, x) * esz)):
+        gb = ids.numel() * (4 + 2 * table_cols(table, x) * esz)
+        with timing.region("embed_gather", 1, gb, gb):
             ops.embed_gather(table, ids, out)
         return out
     if x.dim() != 3:
@@ -122,7 +123,9 @@ def _gru_layer_fwd(cfg, xs, K, ldx, packs, layer, B, T, seeds, want_x1):
     n, H, dt, dev = cfg.ntowers, cfg.H, cfg.dtype, xs[0].device
     BT = B * T
     G = [_alloc((BT, 6 * H), dt, dev) for _ in range(n)]
-    with timing.region(f"input_proj_l{layer}", 1, 2.0 * BT * 6 * H * K * n):
+    esz = 2 if dt == torch.bfloat16 else 4
+    with timing.region(f"input_proj_l{layer}", 1, 2.0 * BT * 6 * H * K * n,
+                       float(n * esz * (BT * K + 6 * H * K + BT * 6 * H))):
         ops.gemm(xs, [p.wih[layer] for p in packs], G, m=BT, n=6 * H, k=K, lda=ldx, ldb=K, ldc=6 * H,
                  a_kouter=False, b_kouter=False, dtype=dt, out_dtype=dt, bias=[p.bias[layer] for p in packs])
     Y = [_alloc((BT, 2 * H), dt, dev) for _ in range(n)]
@@ -143,7 +146,10 @@ def _gru_layer_fwd(cfg, xs, K, ldx, packs, layer, B, T, seeds, want_x1):
             r.dir = d
             r.drop_seed = seeds[ti] & 0xFFFFFFFF
             r.drop_col0 = d * H
-    with timing.region("gru_fwd_step", T, 2.0 * B * H * 3 * H * 2 * n * (T - 1)):
+    # algorithmic bytes per (row, unit): gates 3 + h_{s-1} 1 + h 1 + saved 4 (+ dropout copy 1)
+    # elements of dt, plus the fp32 recurrent state read and written (8 B)
+    with timing.region("gru_fwd_step", T, 2.0 * B * H * 3 * H * 2 * n * (T - 1),
+                       float(B * T * H * 2 * n * (esz * (9 + (1 if want_x1 else 0)) + 8))):
         call("tt_gru_fwd", dtype_code(dt), recs, 2 * n, B, T, H, 6 * H, 2 * H, cfg.drop_p if want_x1 else 0.0,
              stream_ptr(dev))
     del G
@@ -175,7 +181,11 @@ def _gru_layer_bwd(cfg, layer, B, T, S, Y, dY, dfinal, packs):
             r.dbias_part = part[ti * 2 + d].data_ptr()
             r.dir = d
     ldf = dfinal[0].shape[1] if dfinal is not None else 0
-    with timing.region("gru_bwd_step", T, 2.0 * B * 3 * H * H * 2 * n * (T - 1)):
+    # algorithmic bytes per (row, unit): saved 4 + h_{s-1} 1 (+ dY 1) + dgh_{s+1} 3 (GEMM
+    # operand) + dgx 3 + dgh 3 elements of dt, plus the fp32 carry read and written (8 B)
+    esz = 2 if dt == torch.bfloat16 else 4
+    with timing.region("gru_bwd_step", T, 2.0 * B * 3 * H * H * 2 * n * (T - 1),
+                       float(B * T * H * 2 * n * (esz * (14 + (1 if dY is not None else 0)) + 8))):
         call("tt_gru_bwd", dtype_code(dt), recs, 2 * n, B, T, H, 2 * H, 6 * H, ldf, stream_ptr(dev))
     sums = _alloc((n * 2, 4 * H), torch.float32, dev)
     for i in range(2 * n):
@@ -201,10 +211,13 @@ def _weight_grads(cfg, B, T, dG, dGH, Xin, K, ldx, Y):
             b_hh.append(Y[ti][:, d * H:])
             c_hh.append(dWhh[ti][d])
             sh.append(-1 if d == 0 else 1)
-    with timing.region("wgrad_ih", 1, 2.0 * 3 * H * K * BT * 2 * n):
+    esz = 2 if dt == torch.bfloat16 else 4
+    with timing.region("wgrad_ih", 1, 2.0 * 3 * H * K * BT * 2 * n,
+                       float(n * (esz * BT * (6 * H + K) + 2 * 3 * H * K * 4))):
         ops.gemm(a_ih, b_ih, c_ih, m=3 * H, n=K, k=BT, lda=6 * H, ldb=ldx, ldc=K, a_kouter=True, b_kouter=True,
                  dtype=dt, out_dtype=torch.float32)
-    with timing.region("wgrad_hh", 1, 2.0 * 3 * H * H * BT * 2 * n):
+    with timing.region("wgrad_hh", 1, 2.0 * 3 * H * H * BT * 2 * n,
+                       float(n * (esz * BT * (6 * H + 2 * H) + 2 * 3 * H * H * 4))):
         ops.gemm(a_hh, b_hh, c_hh, m=3 * H, n=H, k=BT, lda=6 * H, ldb=2 * H, ldc=H, a_kouter=True, b_kouter=True,
                  dtype=dt, out_dtype=torch.float32, bshift=sh, seq_t=T)
     return dWih, dWhh
@@ -302,7 +315,9 @@ class TowersFn(torch.autograd.Function):
         dWih1, dWhh1 = _weight_grads(cfg, B, T, dG1, dGH1, Xl1, 2 * H, 2 * H, Y1)
         # dL/dY0 = (dG1 Wih1) * dropout mask  [B*T, 2H]
         dY0 = [_alloc((B * T, 2 * H), dt, dev) for _ in range(n)]
-        with timing.region("dgrad_l1", 1, 2.0 * B * T * 2 * H * 6 * H * n):
+        esz = 2 if dt == torch.bfloat16 else 4
+        with timing.region("dgrad_l1", 1, 2.0 * B * T * 2 * H * 6 * H * n,
+                           float(n * esz * (B * T * 6 * H + B * T * 2 * H))):
             if X1 is None:
                 ops.gemm(dG1, [p.wih[1] for p in packs], dY0, m=B * T, n=2 * H, k=6 * H, lda=6 * H, ldb=2 * H,
                          ldc=2 * H, a_kouter=False, b_kouter=True, dtype=dt, out_dtype=dt)

@@ -84,6 +84,30 @@ TT_DEV void st8_sc1(__amdgpu_buffer_rsrc_t r, int off, const float (&f)[8], bf16
   st16_sc1(r, off, make_uint4(w[0], w[1], w[2], w[3]));
 }
 
+// 8 elements held raw (16 B bf16 / 32 B fp32) so loads can be issued long before use.
+template <typename T>
+struct Raw8 {
+  uint4 a, b;
+  TT_DEV void load(const T* p) {
+    a = *reinterpret_cast<const uint4*>(p);
+    if constexpr (sizeof(T) == 4) b = *reinterpret_cast<const uint4*>(p + 4);
+  }
+  TT_DEV void zero() { a = b = make_uint4(0, 0, 0, 0); }
+  TT_DEV void get(float (&f)[8]) const {
+    if constexpr (sizeof(T) == 4) {
+      f[0] = __uint_as_float(a.x); f[1] = __uint_as_float(a.y); f[2] = __uint_as_float(a.z); f[3] = __uint_as_float(a.w);
+      f[4] = __uint_as_float(b.x); f[5] = __uint_as_float(b.y); f[6] = __uint_as_float(b.z); f[7] = __uint_as_float(b.w);
+    } else {
+      const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        f[2 * i] = __uint_as_float(w[i] << 16);
+        f[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+      }
+    }
+  }
+};
+
 TT_DEV float tt_sigmoid(float x) { return 1.0f / (1.0f + __expf(-x)); }
 TT_DEV float tt_tanh(float x) {
   // tanh(x) = 1 - 2/(exp(2x)+1); saturates cleanly for large |x|.

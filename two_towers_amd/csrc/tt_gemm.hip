@@ -45,15 +45,10 @@ struct GemmArgs {
 
 constexpr int BM = 128, BN = 128;  // tile of the register-staged / small path
 
-// XCD-aware order over a 1-D grid: consecutive workgroup ids are dealt round-robin
-// over the 8 XCDs, so remap them (bijectively) to give every XCD a contiguous run of
-// ids. Ids enumerate (batch*split, m-tile, n-tile) with the n-tile fastest, so the
-// tiles of one A panel, and all tiles of one split-K slice, share an XCD's L2.
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  const int xcd = bid & 7, loc = bid >> 3;
-  const int q = nwg >> 3, r = nwg & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
-}
+// 1-D grid in XCD-aware order (ttg::xcd_remap): ids enumerate (batch*split, m-tile,
+// n-tile) with the n-tile fastest, so the tiles of one A panel, and all tiles of one
+// split-K slice, share an XCD's L2.
+using ttg::xcd_remap;
 
 template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO, int TBM, int TBN, int WGM, int WGN, bool DMA>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_kernel(GemmArgs g) {

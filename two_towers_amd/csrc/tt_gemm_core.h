@@ -433,6 +433,15 @@ struct DLoop {
   }
 };
 
+// XCD-aware 1-D workgroup order: ids are dealt round-robin over the 8 XCDs, so remap
+// them (bijectively) to give every XCD a contiguous run; callers enumerate tiles with the
+// fastest index being the one whose tiles share an operand panel.
+TT_DEV int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
 // ---- common loaders ------------------------------------------------------------
 template <typename T>
 struct KCPlain {  // rows [r0, r0+ROWS) of a row-major [rows][ld] matrix

@@ -55,9 +55,14 @@ template <typename T>
 __global__ __launch_bounds__(256) void gru_fwd_step(FwdArgs a) {
   using ML = ttg::DLoop<T, false, false, 128, 192, 2, 2>;
   __shared__ __attribute__((aligned(16))) char lds[ML::LDS_BYTES];
-  const FwdRec R = a.r[blockIdx.z];
+  // 1-D grid, XCD-aware: the H/64 unit tiles of one batch tile are consecutive ids on one
+  // XCD, so its h_{s-1} panel is fetched into that XCD's L2 once, not once per tile.
+  const int ntj = (a.H + 63) / 64, ntm = (a.B + 127) / 128;
+  const int id = ttg::xcd_remap(blockIdx.x, gridDim.x);
+  const int rz = id / (ntm * ntj), rem = id - rz * ntm * ntj;
+  const FwdRec R = a.r[rz];
   const int H = a.H, T_ = a.T, s = a.s;
-  const int m0 = blockIdx.y * 128, j0 = blockIdx.x * 64;
+  const int m0 = (rem / ntj) * 128, j0 = (rem % ntj) * 64;
   const int t = R.dir ? T_ - 1 - s : s;
   const int tp = R.dir ? t + 1 : t - 1;
   const T* Y = static_cast<const T*>(R.y);
@@ -160,9 +165,13 @@ template <typename T>
 __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
   using ML = ttg::DLoop<T, false, true, 128, 128, 2, 2>;
   __shared__ __attribute__((aligned(16))) char lds[ML::LDS_BYTES];
-  const BwdRec R = a.r[blockIdx.z];
+  const int ntj = (a.H + 127) / 128, ntm = (a.B + 127) / 128;
+  const int id = ttg::xcd_remap(blockIdx.x, gridDim.x);
+  const int rz = id / (ntm * ntj), rem = id - rz * ntm * ntj;
+  const int mt = rem / ntj;
+  const BwdRec R = a.r[rz];
   const int H = a.H, T_ = a.T, s = a.s;
-  const int m0 = blockIdx.y * 128, j0 = blockIdx.x * 128;
+  const int m0 = mt * 128, j0 = (rem % ntj) * 128;
   const int t = R.dir ? T_ - 1 - s : s;
   const int tn = R.dir ? t - 1 : t + 1;  // time of step s+1
   const int tp = R.dir ? t + 1 : t - 1;  // time of step s-1
@@ -292,7 +301,7 @@ __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
   }
   __syncthreads();
   if (tid < 128 && j0 + tid < H) {
-    float* pb = R.dbias + (long)blockIdx.y * (4L * H) + j0 + tid;
+    float* pb = R.dbias + (long)mt * (4L * H) + j0 + tid;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       pb[q * H] += red[(0 * 4 + q) * 128 + tid] + red[(1 * 4 + q) * 128 + tid] + red[(2 * 4 + q) * 128 + tid] +
@@ -324,7 +333,7 @@ extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B
   a.drop_thresh = drop_p > 0.f ? (uint32_t)(drop_p * 16777216.0f + 0.5f) : 0u;
   a.inv_keep = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
   hipStream_t st = (hipStream_t)stream;
-  dim3 grid(tt_ceil_div(H, 64), tt_ceil_div(B, 128), nrec);
+  dim3 grid(tt_ceil_div(H, 64) * tt_ceil_div(B, 128) * nrec);
   for (int s = 0; s < T; ++s) {
     a.s = s;
     if (dtype == TT_DT_BF16) hipLaunchKernelGGL(gru_fwd_step<bf16_t>, grid, dim3(256), 0, st, a);
@@ -352,7 +361,7 @@ extern "C" int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B
     TT_CHECK_HIP(hipMemsetAsync(r.dbias_part, 0, sizeof(float) * 4L * H * tt_gru_bias_rows(B), st));
   }
   a.B = B; a.T = T; a.H = H; a.ldy = ldy; a.ldd = ldd; a.ldf = ldf;
-  dim3 grid(tt_ceil_div(H, 128), tt_ceil_div(B, 128), nrec);
+  dim3 grid(tt_ceil_div(H, 128) * tt_ceil_div(B, 128) * nrec);
   for (int s = T - 1; s >= 0; --s) {
     a.s = s;
     if (dtype == TT_DT_BF16) hipLaunchKernelGGL(gru_bwd_step<bf16_t>, grid, dim3(256), 0, st, a);

@@ -101,7 +101,7 @@ typedef struct {
   void* y;             /* h_t: element (b,t,j) at y[(b*T+t)*ldy + j]                 */
   void* x1;            /* optional dropout(y) for the next layer (same layout) or NULL */
   void* save;          /* [B*T, 4H] saved pre-activations of r|z|n and gh_n (backward) */
-  float* hstate;       /* fp32 scratch [2][B][H]                                     */
+  float* hstate;       /* fp32 scratch [2][B][H] (per-step kernel only)              */
   int dir;             /* 0: t = 0..T-1 ; 1: t = T-1..0                              */
   uint32_t drop_seed;  /* dropout stream of x1                                       */
   int drop_col0;       /* column of this recurrence inside the layer output (dir*H)  */
@@ -109,6 +109,10 @@ typedef struct {
 
 int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B, int T, int H, long ldg,
                long ldy, float drop_p, void* stream);
+/* Kernel launches tt_gru_fwd issues: 1 for the persistent bf16 kernel (H % 64 == 0,
+ * H <= 512; 64 batch rows per workgroup kept resident for all T steps, hstate unused),
+ * T for the per-step kernel (fp32, other H, or env TT_GRU_STEP=1). */
+int tt_gru_fwd_launches(int dtype, int T, int H);
 
 /* Backward (BPTT) of tt_gru_fwd. Produces dL/dg (= dgx, feeds dWih, dbih and the
  * layer-input gradient) and dL/dgh (feeds dWhh), plus per-tile bias partial sums

@@ -147,3 +147,27 @@ def test_cpu_tensors_fail_loudly():
     m, _ = make_model(16, 8)
     with pytest.raises(RuntimeError, match="GPU"):
         m(torch.randn(2, 3, 16), torch.randn(2, 3, 16))
+
+
+@pytest.mark.parametrize("h,B,T", [(32, 96, 10), (64, 200, 7), (256, 130, 5)])
+def test_persistent_gru_matches_step_kernel(h, B, T, monkeypatch):
+    """bf16 forward + backward through the persistent (row-resident) GRU forward
+    kernel vs the per-step kernel (env TT_GRU_STEP=1): same arithmetic in the same
+    order, so outputs and gradients agree to fp32 rounding of the gate math."""
+    E = 48
+    g = torch.Generator().manual_seed(11)
+    q = torch.randn(B, T, E, generator=g).to(DEV)
+    d = torch.randn(B, T, E, generator=g).to(DEV)
+    outs = []
+    for step in ("1", "0"):
+        monkeypatch.setenv("TT_GRU_STEP", step)
+        m, _ = make_model(E, h, 3)
+        m = m.to(DEV).train().set_compute_dtype(torch.bfloat16)
+        qv, dv = m(q, d)
+        loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
+        loss.backward()
+        outs.append((qv.detach().clone(), dv.detach().clone(), {k: p.grad.clone() for k, p in m.named_parameters()}))
+    (q0, d0, g0), (q1, d1, g1) = outs
+    assert rel(q1, q0) < 1e-5 and rel(d1, d0) < 1e-5
+    for k in g0:
+        assert rel(g1[k], g0[k]) < 1e-4, k

@@ -1,0 +1,74 @@
+"""Micro-benchmark of tt_gru_fwd / tt_gru_bwd at the bench shape (4 recurrences:
+2 towers x 2 directions), HIP-event timed. Variants via env (TT_GRU_STEP, TT_GRU_DBG)."""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from two_towers_amd import _lib  # noqa: E402
+from two_towers_amd._lib import GruBwdRec, GruFwdRec, call, stream_ptr  # noqa: E402
+
+
+def setup(B, T, H, dev):
+    dt = torch.bfloat16
+    n = 2
+    G = [torch.randn(B * T, 6 * H, device=dev).to(dt) for _ in range(n)]
+    whh = [[(torch.randn(3 * H, H, device=dev) * H ** -0.5).to(dt) for _ in range(2)] for _ in range(n)]
+    bhn = [[torch.randn(H, device=dev) * 0.1 for _ in range(2)] for _ in range(n)]
+    Y = [torch.empty(B * T, 2 * H, device=dev, dtype=dt) for _ in range(n)]
+    X1 = [torch.empty(B * T, 2 * H, device=dev, dtype=dt) for _ in range(n)]
+    S = [[torch.empty(B * T, 4 * H, device=dev, dtype=dt) for _ in range(2)] for _ in range(n)]
+    hs = [torch.empty(2, B, H, device=dev) for _ in range(2 * n)]
+    recs = (GruFwdRec * (2 * n))()
+    for ti in range(n):
+        for d in range(2):
+            r = recs[ti * 2 + d]
+            r.g = G[ti][:, d * 3 * H:].data_ptr()
+            r.whh = whh[ti][d].data_ptr()
+            r.bhn = bhn[ti][d].data_ptr()
+            r.y = Y[ti][:, d * H:].data_ptr()
+            r.x1 = X1[ti][:, d * H:].data_ptr()
+            r.save = S[ti][d].data_ptr()
+            r.hstate = hs[ti * 2 + d].data_ptr()
+            r.dir = d
+            r.drop_seed = 7 + ti
+            r.drop_col0 = d * H
+    keep = (G, whh, bhn, Y, X1, S, hs)
+    return recs, keep
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=8192)
+    ap.add_argument("--T", type=int, default=64)
+    ap.add_argument("--H", type=int, default=512)
+    ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--variants", default="step:0,seq:0:4,seq:1:4,seq:3:4,seq:16:4,seq:19:4")
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    recs, keep = setup(a.B, a.T, a.H, dev)
+    st = stream_ptr(dev)
+    for v in a.variants.split(","):
+        kind, dbg, *depth = v.split(":")
+        os.environ["TT_GRU_STEP"] = "1" if kind == "step" else "0"
+        os.environ["TT_GRU_DBG"] = dbg
+        os.environ["TT_GRU_DEPTH"] = depth[0] if depth else "4"
+        f = lambda: call("tt_gru_fwd", 1, recs, 4, a.B, a.T, a.H, 6 * a.H, 2 * a.H, 0.1, st)
+        f()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.iters):
+            f()
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / a.iters
+        gb = a.B * a.T * a.H * 4 * 18 / 1e9
+        print(json.dumps({"variant": v, "ms": round(ms, 3), "alg_GBs_18B": round(gb / (ms * 1e-3), 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -10,6 +10,7 @@
 // are ordered [unit half][gate][32 units] so that every lane holds r, z and n for
 // the same (b, j) in registers and the update needs no data exchange.
 #include <algorithm>
+#include <cstdlib>
 
 #include "tt_api.h"
 #include "tt_gemm_core.h"
@@ -27,6 +28,7 @@ struct FwdArgs {
   int s;
   uint32_t drop_thresh;
   float inv_keep;
+  int dbg;  // diagnostics (env TT_GRU_DBG): 1 no stores, 2 no G loads, 4 no MFMA, 8 no Whh stream
 };
 
 struct BwdRec {
@@ -309,9 +311,259 @@ __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
   }
 }
 
+// ---- persistent ("row-resident") forward, bf16 ---------------------------------
+// Batch rows never interact, so one workgroup can own 64 rows of one recurrence for
+// all T steps: h_{s-1} stays in LDS as the A operand (bf16 KC image, never re-read
+// from HBM), the fp32 state h_s stays in registers, and only Whh (1.5 MiB per
+// recurrence at H=512, L2-resident) is streamed per step. HBM traffic per (row, unit,
+// step) drops to what the recurrence must read (G) and write (Y, saved
+// pre-activations, dropout copy): 16-18 B instead of 28 B, in one launch instead of T.
+//   LDS: Hb 64 KiB (64 rows x H<=512 bf16) | 2 x 24 KiB Whh K-tiles | 48 KiB fp32 gates
+// Per step, per block of 64 hidden units: GEMM [64 x 192] += Hb[64 x H] Whh_blk^T
+// (8 waves as 2 x 4, wave tile 32 x 48), gates staged through LDS, then every thread
+// updates 8 consecutive units of one row with 16-byte global accesses.
+constexpr int PR = 64, PH_MAX = 512, PNT = 512;
+constexpr int P_HB = PR * PH_MAX * 2;      // 65536
+constexpr int P_BST = 192 * ttg::KTB;      // 24576 per stage
+constexpr int P_STG = PR * 192 * 4;        // 49152
+constexpr int P_LDS = P_HB + 2 * P_BST + P_STG;
+static_assert(P_LDS <= 163840, "persistent GRU LDS budget");
+
+// fp32 gate tile [64 rows][48 chunks of 4]: chunk c of row r at c ^ (r & 15)
+// (conflict-free for the MFMA-layout writes and the 8-float row reads below).
+TT_DEV void unpack8(uint4 v, float (&f)[8]) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xFFFF0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xFFFF0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xFFFF0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xFFFF0000u);
+}
+
+TT_DEV int stg_off(int row, int col) { return row * 192 + ((((col >> 2) ^ (row & 15))) << 2) + (col & 3); }
+
+// Whh K-tile q = blk*(H/64) + kt of a step, B-tile row (g*64 + u) -> Whh row
+// g*H + blk*64 + u; 3 chunks of 16 B per thread.
+struct WTile {
+  uint4 v0, v1, v2;
+};
+TT_DEV uint4 fwd_load_chunk(const bf16_t* W, int H, int blk, int kt, int i) {
+  const int id = threadIdx.x + PNT * i, c = id & 7, row = id >> 3;
+  const int g = row >> 6, u = row & 63;
+  return *reinterpret_cast<const uint4*>(W + (long)(g * H + blk * 64 + u) * H + kt * 64 + c * 8);
+}
+TT_DEV void fwd_load_b(const bf16_t* W, int H, int q, WTile& r) {
+  const int nkt = H >> 6, blk = q / nkt, kt = q - blk * nkt;
+  r.v0 = fwd_load_chunk(W, H, blk, kt, 0);
+  r.v1 = fwd_load_chunk(W, H, blk, kt, 1);
+  r.v2 = fwd_load_chunk(W, H, blk, kt, 2);
+}
+TT_DEV void fwd_store_b(char* img, const WTile& r) {
+  const int t = threadIdx.x;
+  *reinterpret_cast<uint4*>(img + ttg::kc_off(t >> 3, t & 7)) = r.v0;
+  *reinterpret_cast<uint4*>(img + ttg::kc_off((t + PNT) >> 3, t & 7)) = r.v1;
+  *reinterpret_cast<uint4*>(img + ttg::kc_off((t + 2 * PNT) >> 3, t & 7)) = r.v2;
+}
+// One K-tile of the step GEMM: prefetch K-tile q+D into register set Y (wrapping into
+// the next step; the very last prefetches are harmless reloads, unconditional so the
+// sets stay in registers), MFMAs on LDS stage it&1, then K-tile q+1 (set X, loaded
+// D-1 tiles ago) into the other stage.
+template <int D>
+TT_DEV void fwd_kstep(const bf16_t* W, int H, int Q, int q, int kt, bool mm, const char* hb, char* bst, int& it,
+                      int wm, int wn, f32x4 (&acc)[2][3], WTile& X, WTile& Y) {
+  fwd_load_b(W, H, (q + D) % Q, Y);
+  if (mm) {  // h_{-1} = 0: the first step has no recurrent term
+    const char* ia = hb + kt * (PR * ttg::KTB);
+    const char* ib = bst + (it & 1) * P_BST;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 fa[2], fb[3];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = ttg::frag<bf16_t, false>(ia, wm + 16 * i, ks);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) fb[j] = ttg::frag<bf16_t, false>(ib, wn + 16 * j, ks);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[i][j] = ttg::mma<bf16_t>(fa[i], fb[j], acc[i][j]);
+    }
+  }
+  fwd_store_b(bst + ((it + 1) & 1) * P_BST, X);
+  __syncthreads();
+  ++it;
+}
+
+template <int D>  // Whh K-tiles in flight in registers: 1, 2 or 4 (D divides H/64)
+__global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[P_LDS];
+  char* hb = lds;
+  char* bst = lds + P_HB;
+  float* stg = reinterpret_cast<float*>(lds + P_HB + 2 * P_BST);
+  const int ntm = (a.B + PR - 1) / PR;
+  const int id = ttg::xcd_remap(blockIdx.x, gridDim.x);
+  const int rz = id / ntm;
+  const FwdRec R = a.r[rz];
+  const int H = a.H, T_ = a.T;
+  const int m0 = (id - rz * ntm) * PR;
+  const int nblk = H / 64, nkt = H / 64, Q = nblk * nkt;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = (wave >> 2) * 32, wn = (wave & 3) * 48;
+  const bf16_t* W = static_cast<const bf16_t*>(R.whh);
+  const bf16_t* G = static_cast<const bf16_t*>(R.g);
+  bf16_t* Yw = static_cast<bf16_t*>(R.y);
+  bf16_t* X1 = static_cast<bf16_t*>(R.x1);
+  bf16_t* S = static_cast<bf16_t*>(R.save);
+  // epilogue ownership: row rl, units blk*64 + jg .. +8 of every block
+  const int rl = tid >> 3, jg = (tid & 7) * 8;
+  const int b = m0 + rl;
+  const bool rowok = b < a.B;
+
+  float hreg[PH_MAX / 64][8];
+#pragma unroll
+  for (int i = 0; i < PH_MAX / 64; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) hreg[i][e] = 0.f;
+
+  WTile r0, r1, r2, r3;
+  fwd_load_b(W, H, 0, r0);
+  fwd_store_b(bst, r0);
+  if (D >= 2) fwd_load_b(W, H, 1 % Q, r1);
+  if (D >= 4) {
+    fwd_load_b(W, H, 2 % Q, r2);
+    fwd_load_b(W, H, 3 % Q, r3);
+  }
+  int it = 0;  // running K-tile counter: Whh stage = it & 1
+  __syncthreads();
+
+  for (int s = 0; s < T_; ++s) {
+    const int t = R.dir ? T_ - 1 - s : s;
+    const long row = (long)b * T_ + t;
+#pragma unroll
+    for (int blk = 0; blk < nblk; ++blk) {
+      {
+        // gate inputs of this block's epilogue, issued before the GEMM so they land under it
+        uint4 gx[3];
+        if (rowok && !(a.dbg & 2)) {
+#pragma unroll
+          for (int g = 0; g < 3; ++g)
+            gx[g] = *reinterpret_cast<const uint4*>(G + row * a.ldg + g * H + blk * 64 + jg);
+        } else {
+#pragma unroll
+          for (int g = 0; g < 3; ++g) gx[g] = make_uint4(0, 0, 0, 0);
+        }
+        f32x4 acc[2][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // ring of D register sets: iteration q reads set (q+1)%D, refills set q%D
+#define TT_KS(j, X, Y) fwd_kstep<D>(W, H, Q, blk * nkt + kt + j, kt + j, s > 0, hb, bst, it, wm, wn, acc, X, Y)
+        if constexpr (D == 1) {
+          for (int kt = 0; kt < nkt; ++kt) TT_KS(0, r0, r0);
+        } else if constexpr (D == 2) {
+          for (int kt = 0; kt < nkt; kt += 2) { TT_KS(0, r1, r0); TT_KS(1, r0, r1); }
+        } else {
+          for (int kt = 0; kt < nkt; kt += 4) { TT_KS(0, r1, r0); TT_KS(1, r2, r1); TT_KS(2, r3, r2); TT_KS(3, r0, r3); }
+        }
+#undef TT_KS
+        // gates -> LDS (fp32), then per-thread rows
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              stg[stg_off(wm + 16 * i + 4 * (lane >> 4) + r, wn + 16 * j + (lane & 15))] = acc[i][j][r];
+        __syncthreads();
+        const int j = blk * 64 + jg;
+        float xr[8], xz[8], xn[8], bn[8], lr[8], lz[8], ln[8], y[8], sr[8], sz[8], sn[8], sg[8];
+        unpack8(gx[0], xr);
+        unpack8(gx[1], xz);
+        unpack8(gx[2], xn);
+        ld8(R.bhn + j, bn);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float4 v0 = *reinterpret_cast<const float4*>(stg + stg_off(rl, 0 * 64 + jg + 4 * h));
+          const float4 v1 = *reinterpret_cast<const float4*>(stg + stg_off(rl, 1 * 64 + jg + 4 * h));
+          const float4 v2 = *reinterpret_cast<const float4*>(stg + stg_off(rl, 2 * 64 + jg + 4 * h));
+          lr[4 * h] = v0.x; lr[4 * h + 1] = v0.y; lr[4 * h + 2] = v0.z; lr[4 * h + 3] = v0.w;
+          lz[4 * h] = v1.x; lz[4 * h + 1] = v1.y; lz[4 * h + 2] = v1.z; lz[4 * h + 3] = v1.w;
+          ln[4 * h] = v2.x; ln[4 * h + 1] = v2.y; ln[4 * h + 2] = v2.z; ln[4 * h + 3] = v2.w;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float ghn = ln[e] + bn[e];
+          const float ar = xr[e] + lr[e], az = xz[e] + lz[e];
+          const float rg = tt_sigmoid(ar), zg = tt_sigmoid(az);
+          const float an = xn[e] + rg * ghn;
+          const float ng = tt_tanh(an);
+          y[e] = (1.f - zg) * ng + zg * hreg[0][e];
+          sr[e] = ar; sz[e] = az; sn[e] = an; sg[e] = ghn;
+        }
+        float ynew[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ynew[e] = y[e];
+        if (rowok && !(a.dbg & 1)) {
+          st8(Yw + row * a.ldy + j, y);
+          bf16_t* sp = S + row * (4L * H) + j;
+          st8(sp, sr);
+          st8(sp + H, sz);
+          st8(sp + 2 * H, sn);
+          st8(sp + 3 * H, sg);
+          if (X1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              y[e] *= a.drop_thresh ? tt_dropout_scale(R.seed, (uint32_t)row, (uint32_t)(R.col0 + j + e),
+                                                       a.drop_thresh, a.inv_keep)
+                                    : 1.f;
+            st8(X1 + row * a.ldy + j, y);
+          }
+        }
+        // stg is rewritten only after the next block's K loop (whose barriers order it)
+        // the state of block blk moves to the back: hreg[0] is always the current block
+#pragma unroll
+        for (int i = 0; i < PH_MAX / 64 - 1; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) hreg[i][e] = hreg[i + 1][e];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) hreg[PH_MAX / 64 - 1][e] = ynew[e];
+      }
+    }
+    for (int r = nblk; r < PH_MAX / 64; ++r) {  // complete the rotation: hreg[b] = block b
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = hreg[0][e];
+#pragma unroll
+        for (int i = 0; i < PH_MAX / 64 - 1; ++i) hreg[i][e] = hreg[i + 1][e];
+        hreg[PH_MAX / 64 - 1][e] = v;
+      }
+    }
+    // h_s -> A operand of step s+1 (every wave finished reading h_{s-1}: the last
+    // K-tile ended with a barrier)
+#pragma unroll
+    for (int blk = 0; blk < PH_MAX / 64; ++blk) {
+      if (blk < nblk) {
+        uint32_t w[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          w[i] = (uint32_t)f2bf(hreg[blk][2 * i]) | ((uint32_t)f2bf(hreg[blk][2 * i + 1]) << 16);
+        *reinterpret_cast<uint4*>(hb + blk * (PR * ttg::KTB) + ttg::kc_off(rl, tid & 7)) =
+            make_uint4(w[0], w[1], w[2], w[3]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+bool gru_fwd_persistent(int dtype, int H) {
+  if (dtype != TT_DT_BF16 || H % 64 != 0 || H > PH_MAX) return false;
+  const char* e = getenv("TT_GRU_STEP");
+  return !(e && e[0] == '1');
+}
+
 }  // namespace
 
 extern "C" int tt_gru_bias_rows(int B) { return tt_ceil_div(B, 128); }
+
+extern "C" int tt_gru_fwd_launches(int dtype, int T, int H) { return gru_fwd_persistent(dtype, H) ? 1 : T; }
 
 extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B, int T, int H, long ldg,
                           long ldy, float drop_p, void* stream) {
@@ -332,7 +584,18 @@ extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B
   a.B = B; a.T = T; a.H = H; a.ldg = ldg; a.ldy = ldy;
   a.drop_thresh = drop_p > 0.f ? (uint32_t)(drop_p * 16777216.0f + 0.5f) : 0u;
   a.inv_keep = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
+  if (const char* e = getenv("TT_GRU_DBG")) a.dbg = atoi(e);
   hipStream_t st = (hipStream_t)stream;
+  if (gru_fwd_persistent(dtype, H)) {
+    const dim3 grid(tt_ceil_div(B, PR) * nrec);
+    int depth = (H / 64) % 4 == 0 ? 4 : (H / 64) % 2 == 0 ? 2 : 1;
+    if (const char* e = getenv("TT_GRU_DEPTH")) depth = std::min(depth, atoi(e));
+    if (depth >= 4) hipLaunchKernelGGL(gru_fwd_seq<4>, grid, dim3(PNT), 0, st, a);
+    else if (depth == 2) hipLaunchKernelGGL(gru_fwd_seq<2>, grid, dim3(PNT), 0, st, a);
+    else hipLaunchKernelGGL(gru_fwd_seq<1>, grid, dim3(PNT), 0, st, a);
+    TT_CHECK_LAUNCH("gru_fwd_seq");
+    return 0;
+  }
   dim3 grid(tt_ceil_div(H, 64) * tt_ceil_div(B, 128) * nrec);
   for (int s = 0; s < T; ++s) {
     a.s = s;

@@ -52,8 +52,11 @@ using ttg::xcd_remap;
 
 template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO, int TBM, int TBN, int WGM, int WGN, bool DMA>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_kernel(GemmArgs g) {
-  using ML = std::conditional_t<DMA, ttg::DLoop<T, AKO, BKO, TBM, TBN, WGM, WGN>,
-                                ttg::MainLoop<T, AKO, BKO, TBM, TBN>>;
+  using ML = std::conditional_t<
+      DMA,
+      std::conditional_t<TBM == 256 && TBN == 256 && WGM == 2 && WGN == 4, ttg::Loop8<T, AKO, BKO>,
+                         ttg::DLoop<T, AKO, BKO, TBM, TBN, WGM, WGN>>,
+      ttg::MainLoop<T, AKO, BKO, TBM, TBN>>;
   static_assert(DMA || (TBM == 128 && TBN == 128 && WGM == 2 && WGN == 2), "register path is 128x128");
   constexpr int NT = 64 * WGM * WGN;
   constexpr int LDSB = ML::LDS_BYTES > 64 * (TBN + 4) * 4 ? ML::LDS_BYTES : 64 * (TBN + 4) * 4;

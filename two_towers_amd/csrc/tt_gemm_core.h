@@ -433,6 +433,167 @@ struct DLoop {
   }
 };
 
+// ---- 256x256 8-phase LDS-DMA loop (8 waves as 2M x 4N, wave tile 128 x 64) ----------
+// The tile's A and B K-tiles are staged as four 16 KiB half-tiles (A rows 0-127 / 128-255,
+// B columns 0-127 / 128-255) into two LDS slots (128 KiB). Each K-tile runs 4 phases, one
+// 64x32 accumulator quadrant (16 MFMAs) each, with one half-tile DMA issued per phase:
+//   P1: read A(rows 0-63 of the wave) + all B fragments; DMA A0 of K-tile t+1
+//   P2: DMA A1 of t+1
+//   P3: read A(rows 64-127); DMA B0 of t+2 into the current slot (B last read in P1)
+//   P4: DMA B1 of t+2; s_waitcnt vmcnt(4) -> K-tile t+1 has landed
+// The two wave rows (wr = 0, 1) run one barrier apart, so one group's fragment reads
+// and DMA issue overlap the other group's MFMAs; every restage is >= 2 phases after the
+// last read of its half-tile and every read >= 1 barrier after the wait that retired it,
+// with the one extra barrier the stagger needs (recipe: cdna_hip_programming.md §5, the
+// 256^2 8-phase template: counted vmcnt, raw s_barrier, all LDS in one array). Every wave
+// issues 2 DMAs per half-tile, always (a K-tile past the slice end reads the zero page),
+// so the counts are exact.
+template <typename T, bool AKO, bool BKO>
+struct Loop8 {
+  static constexpr int HALF = 16384, SLOT = 4 * HALF, LDS_BYTES = 2 * SLOT;
+  static constexpr int TM = 8, TN = 4;
+  static constexpr int KTE = KTB / (int)sizeof(T);  // K elements per K-tile
+
+  // One thread's two 1 KiB pieces of a half-tile, resolved once per tile: the source
+  // address at K-tile kt0 plus the number of K-tiles for which the piece is in range
+  // (K tail, M/N tail and slice end folded together), so a DMA issue costs a 64-bit add,
+  // a compare and a select instead of re-deriving the row/column address every K-tile.
+  struct Piece {
+    const char* p;  // source at K-tile kt0 (any valid address when lim == 0)
+    int lim;        // in range for relative K-tiles [0, lim)
+    int t0;         // KOShift: time index of the piece's k-row at kt0
+  };
+  template <bool KO, class L>
+  TT_DEV static void init_half(const L& ld, int kt0, int ktl, int K, int roff, Piece (&pc)[2]) {
+    constexpr int EPC = Elt<T>::EPC;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int p = (wave + 8 * j) * 64 + lane;
+      pc[j].p = reinterpret_cast<const char*>(g_tt_zero_page);
+      pc[j].lim = 0;
+      pc[j].t0 = 0;
+      if constexpr (!KO) {
+        const int row = p >> 3;
+        const int c = (p & 7) ^ ((row >> 1) & 7);
+        const T* rp = ld.rowptr(roff + row);
+        const int k0 = kt0 * KTE + c * EPC;
+        if (rp != nullptr) {
+          pc[j].p = reinterpret_cast<const char*>(rp + k0);
+          pc[j].lim = min(ktl - kt0, (K - k0 + KTE - 1) / KTE);
+        }
+      } else {
+        constexpr int CPR = 128 * (int)sizeof(T) / 16;
+        const int kl = p / CPR, q = p % CPR;
+        int c;
+        if constexpr (sizeof(T) == 2) c = q ^ (ko_v(kl) << 1);
+        else c = q ^ (((kl >> 2) & 1) << 2);
+        const int col = roff + c * EPC;
+        const int k0 = kt0 * KTE + kl;
+        if (col < ld.ncols && k0 < K) {
+          pc[j].p = reinterpret_cast<const char*>(ld.base + (long)k0 * ld.ld + ld.c0 + col);
+          pc[j].lim = min(ktl - kt0, (K - k0 + KTE - 1) / KTE);
+          if constexpr (L::SHIFTED) pc[j].t0 = k0 % ld.T_;
+        }
+      }
+    }
+  }
+  // DMA relative K-tile r of a half-tile (delta = bytes between consecutive K-tiles).
+  template <class L>
+  TT_DEV static void issue_half(const L& ld, const Piece (&pc)[2], int r, long delta, uint32_t img) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int dt = 0;
+    if constexpr (L::SHIFTED) dt = (int)(((long)r * KTE) % ld.T_);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bool ok = r < pc[j].lim;
+      long off = (long)r * delta;
+      if constexpr (L::SHIFTED) {
+        int t = pc[j].t0 + dt;
+        t -= t >= ld.T_ ? ld.T_ : 0;
+        const int ts = t + ld.shift;
+        ok = ok && ts >= 0 && ts < ld.T_;
+        off += (long)ld.shift * ld.ld * (long)sizeof(T);
+      }
+      const char* src = ok ? pc[j].p + off : reinterpret_cast<const char*>(g_tt_zero_page);
+      dma16(src, img + (uint32_t)(wave + 8 * j) * 1024u);
+    }
+  }
+  TT_DEV static void quad(int mi, int ni, const uint4 (&fa)[2][4], const uint4 (&fb)[2][4], f32x4 (&acc)[TM][TN]) {
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 * mi + i][2 * ni + j] = mma<T>(fa[ks][i], fb[ks][2 * ni + j], acc[4 * mi + i][2 * ni + j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+  }
+
+  template <class LA, class LB>
+  TT_DEV static void run(const LA& la, const LB& lb, int K, int kt0, int kt1, char* lds, f32x4 (&acc)[TM][TN]) {
+    if (kt0 >= kt1) return;
+    const int wave = threadIdx.x >> 6;
+    const int wr = wave >> 2, bh = (wave & 3) >> 1, bc = (wave & 1) * 64;
+    const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr_of(lds));
+    Piece pa0[2], pa1[2], pb0[2], pb1[2];
+    init_half<AKO>(la, kt0, kt1, K, 0, pa0);
+    init_half<AKO>(la, kt0, kt1, K, 128, pa1);
+    init_half<BKO>(lb, kt0, kt1, K, 0, pb0);
+    init_half<BKO>(lb, kt0, kt1, K, 128, pb1);
+    long da = KTB, db = KTB;  // K-contig operands advance 128 B per K-tile
+    if constexpr (AKO) da = (long)KTE * la.ld * (long)sizeof(T);
+    if constexpr (BKO) db = (long)KTE * lb.ld * (long)sizeof(T);
+    issue_half(la, pa0, 0, da, base);
+    issue_half(la, pa1, 0, da, base + HALF);
+    issue_half(lb, pb0, 0, db, base + 2 * HALF);
+    issue_half(lb, pb1, 0, db, base + 3 * HALF);
+    issue_half(lb, pb0, 1, db, base + SLOT + 2 * HALF);
+    issue_half(lb, pb1, 1, db, base + SLOT + 3 * HALF);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const bool late = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;  // wave row 1
+    if (late) __builtin_amdgcn_s_barrier();
+    uint4 fa[2][4], fb[2][4];
+    for (int r = 0; r < kt1 - kt0; ++r) {
+      const int cs = r & 1;
+      const uint32_t cur = base + cs * SLOT, nxt = base + (cs ^ 1) * SLOT;
+      const char* ia = lds + cs * SLOT + wr * HALF;
+      const char* ib = lds + cs * SLOT + (2 + bh) * HALF;
+      // P1
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[ks][i] = frag2<T, AKO>(ia, 16 * i, ks);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[ks][j] = frag2<T, BKO>(ib, bc + 16 * j, ks);
+      }
+      issue_half(la, pa0, r + 1, da, nxt);
+      quad(0, 0, fa, fb, acc);
+      // P2
+      issue_half(la, pa1, r + 1, da, nxt + HALF);
+      quad(0, 1, fa, fb, acc);
+      // P3
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[ks][i] = frag2<T, AKO>(ia, 64 + 16 * i, ks);
+      issue_half(lb, pb0, r + 2, db, cur + 2 * HALF);
+      quad(1, 1, fa, fb, acc);
+      // P4
+      issue_half(lb, pb1, r + 2, db, cur + 3 * HALF);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      quad(1, 0, fa, fb, acc);
+    }
+    if (!late) __builtin_amdgcn_s_barrier();  // re-align the two wave rows
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing zero-page DMAs before LDS reuse
+    __builtin_amdgcn_s_barrier();
+  }
+};
+
 // XCD-aware 1-D workgroup order: ids are dealt round-robin over the 8 XCDs, so remap
 // them (bijectively) to give every XCD a contiguous run; callers enumerate tiles with the
 // fastest index being the one whose tiles share an operand panel.
@@ -445,11 +606,13 @@ TT_DEV int xcd_remap(int bid, int nwg) {
 // ---- common loaders ------------------------------------------------------------
 template <typename T>
 struct KCPlain {  // rows [r0, r0+ROWS) of a row-major [rows][ld] matrix
+  static constexpr bool SHIFTED = false;
   const T* base; long ld; int r0, rows;
   TT_DEV const T* rowptr(int r) const { int g = r0 + r; return g < rows ? base + (long)g * ld : nullptr; }
 };
 template <typename T>
 struct KOPlain {  // columns [c0, c0+128) of a row-major [K][ld] matrix
+  static constexpr bool SHIFTED = false;
   const T* base; long ld; int c0, ncols;
   TT_DEV const T* kptr(int k) const { return base + (long)k * ld + c0; }
 };
@@ -457,6 +620,7 @@ struct KOPlain {  // columns [c0, c0+128) of a row-major [K][ld] matrix
 // zero when t+shift falls outside [0,T). Used for the GRU h_{s-1} operand of dW_hh.
 template <typename T>
 struct KOShift {
+  static constexpr bool SHIFTED = true;
   const T* base; long ld; int c0, ncols, T_, shift;
   TT_DEV const T* kptr(int k) const {
     const int t = k % T_;

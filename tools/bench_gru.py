@@ -40,17 +40,66 @@ def setup(B, T, H, dev):
     return recs, keep
 
 
+def setup_bwd(B, T, H, keep, dev):
+    dt = torch.bfloat16
+    G, whh, bhn, Y, X1, S, hs = keep
+    n = 2
+    dY = [torch.randn(B * T, 2 * H, device=dev).to(dt) * 0.01 for _ in range(n)]
+    dfin = [torch.randn(B, 2 * H, device=dev) * 0.01 for _ in range(n)]
+    dG = [torch.empty(B * T, 6 * H, device=dev, dtype=dt) for _ in range(n)]
+    dGH = [torch.empty(B * T, 6 * H, device=dev, dtype=dt) for _ in range(n)]
+    dhs = [torch.empty(2, B, H, device=dev) for _ in range(2 * n)]
+    nbr = _lib.load().tt_gru_bias_rows(B)
+    part = [torch.empty(nbr, 4 * H, device=dev) for _ in range(2 * n)]
+    recs = (GruBwdRec * (2 * n))()
+    for ti in range(n):
+        for d in range(2):
+            r = recs[ti * 2 + d]
+            r.save = S[ti][d].data_ptr()
+            r.y = Y[ti][:, d * H:].data_ptr()
+            r.dy = dY[ti][:, d * H:].data_ptr()
+            r.dfinal = dfin[ti][:, d * H:].data_ptr()
+            r.whh = whh[ti][d].data_ptr()
+            r.dgx = dG[ti][:, d * 3 * H:].data_ptr()
+            r.dgh = dGH[ti][:, d * 3 * H:].data_ptr()
+            r.dhstate = dhs[ti * 2 + d].data_ptr()
+            r.dbias_part = part[ti * 2 + d].data_ptr()
+            r.dir = d
+    return recs, (dY, dfin, dG, dGH, dhs, part)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--B", type=int, default=8192)
     ap.add_argument("--T", type=int, default=64)
     ap.add_argument("--H", type=int, default=512)
     ap.add_argument("--iters", type=int, default=3)
-    ap.add_argument("--variants", default="step:0,seq:0:4,seq:1:4,seq:3:4,seq:16:4,seq:19:4")
+    ap.add_argument("--variants", default="seq:0")
+    ap.add_argument("--bwd-variants", default="128:0:1,128:0:2,64:0:2")
     a = ap.parse_args()
     dev = torch.device("cuda")
     recs, keep = setup(a.B, a.T, a.H, dev)
     st = stream_ptr(dev)
+    for v in a.bwd_variants.split(","):
+        if not v:
+            continue
+        rows, dbg, strm = (v.split(":") + ["0", "2"])[:3]
+        os.environ["TT_GRU_BWD_ROWS"] = rows
+        os.environ["TT_GRU_DBG"] = dbg
+        os.environ["TT_GRU_BWD_STREAMS"] = strm
+        brecs, bkeep = setup_bwd(a.B, a.T, a.H, keep, dev)
+        f = lambda: call("tt_gru_bwd", 1, brecs, 4, a.B, a.T, a.H, 2 * a.H, 6 * a.H, 2 * a.H, st)
+        f()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.iters):
+            f()
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / a.iters
+        print(json.dumps({"bwd_rows": v, "ms": round(ms, 3)}), flush=True)
+        del brecs, bkeep
     for v in a.variants.split(","):
         kind, dbg, *depth = v.split(":")
         os.environ["TT_GRU_STEP"] = "1" if kind == "step" else "0"

@@ -40,6 +40,7 @@ struct BwdArgs {
   int B, T, H;
   long ldy, ldd, ldf;
   int s;
+  int dbg;  // timing diagnostics only (env TT_GRU_DBG): 32 skips the GEMM, 64 the epilogue
 };
 
 // B-tile row r of the forward step -> row (gate*H + j) of Whh [3H, H].
@@ -163,17 +164,18 @@ __global__ __launch_bounds__(256) void gru_fwd_step(FwdArgs a) {
   }
 }
 
-template <typename T>
+template <typename T, int BMR>  // BMR batch rows per tile: 128, or 64 (3 tiles per CU)
 __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
-  using ML = ttg::DLoop<T, false, true, 128, 128, 2, 2>;
-  __shared__ __attribute__((aligned(16))) char lds[ML::LDS_BYTES];
-  const int ntj = (a.H + 127) / 128, ntm = (a.B + 127) / 128;
+  using ML = ttg::DLoop<T, false, true, BMR, 128, 2, 2>;
+  constexpr int LDSB = ML::LDS_BYTES > 64 * 132 * 4 ? ML::LDS_BYTES : 64 * 132 * 4;
+  __shared__ __attribute__((aligned(16))) char lds[LDSB];
+  const int ntj = (a.H + 127) / 128, ntm = (a.B + BMR - 1) / BMR;
   const int id = ttg::xcd_remap(blockIdx.x, gridDim.x);
   const int rz = id / (ntm * ntj), rem = id - rz * ntm * ntj;
   const int mt = rem / ntj;
   const BwdRec R = a.r[rz];
   const int H = a.H, T_ = a.T, s = a.s;
-  const int m0 = mt * 128, j0 = (rem % ntj) * 128;
+  const int m0 = mt * BMR, j0 = (rem % ntj) * 128;
   const int t = R.dir ? T_ - 1 - s : s;
   const int tn = R.dir ? t - 1 : t + 1;  // time of step s+1
   const int tp = R.dir ? t + 1 : t - 1;  // time of step s-1
@@ -185,7 +187,7 @@ __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
   for (int i = 0; i < ML::TM; ++i)
 #pragma unroll
     for (int j = 0; j < ML::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (!last) {
+  if (!last && !(a.dbg & 32)) {
     ttg::KCPlain<T> la{DGH + (long)tn * a.ldd, (long)T_ * a.ldd, m0, a.B};
     ttg::KOPlain<T> lb{static_cast<const T*>(R.whh), H, j0, H - j0};
     const int K = 3 * H;
@@ -193,6 +195,10 @@ __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
     ML::run(la, lb, K, 0, nk, lds, acc);
   }
 
+  if (a.dbg & 64) {
+    if (threadIdx.x == 0 && acc[0][0][0] == 12345.f) R.dbias[0] = 1.f;  // keep the GEMM live
+    return;
+  }
   // ---- epilogue, one 64-row half at a time through LDS; each thread owns 8
   // consecutive units of a row (16-byte accesses) for 4 rows per half.
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, tid = threadIdx.x;
@@ -215,16 +221,18 @@ __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
   for (int q = 0; q < 4; ++q)
 #pragma unroll
     for (int e = 0; e < 8; ++e) bsum[q][e] = 0.f;
-  for (int hf = 0; hf < 2; ++hf) {
-    if ((wave >> 1) == hf) {
+  for (int hf = 0; hf < BMR / 64; ++hf) {
+    // waves whose accumulator rows fall in this 64-row slice stage them
+    const int wrow = (wave >> 1) * (BMR / 2) - hf * 64;
+    if (wrow >= 0 && wrow < 64) {
       const int wn = (wave & 1) * 64;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < ML::TM; ++i)
 #pragma unroll
         for (int jt = 0; jt < 4; ++jt)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            L[(16 * i + 4 * (lane >> 4) + r) * BLD + wn + 16 * jt + (lane & 15)] = acc[i][jt][r];
+            L[(wrow + 16 * i + 4 * (lane >> 4) + r) * BLD + wn + 16 * jt + (lane & 15)] = acc[i][jt][r];
     }
     __syncthreads();
 #pragma unroll
@@ -561,9 +569,35 @@ bool gru_fwd_persistent(int dtype, int H) {
 
 }  // namespace
 
-extern "C" int tt_gru_bias_rows(int B) { return tt_ceil_div(B, 128); }
+// batch rows per backward tile: 128, or 64 with env TT_GRU_BWD_ROWS=64 (3 workgroups
+// per CU; measured slower at B=8192, H=512: 13.6 vs 11.5 ms per layer)
+static int bwd_rows() {
+  const char* e = getenv("TT_GRU_BWD_ROWS");
+  return (e && atoi(e) == 64) ? 64 : 128;
+}
+extern "C" int tt_gru_bias_rows(int B) { return tt_ceil_div(B, bwd_rows()); }
 
 extern "C" int tt_gru_fwd_launches(int dtype, int T, int H) { return gru_fwd_persistent(dtype, H) ? 1 : T; }
+
+// Per-device side stream + fork/join events for tt_gru_bwd's second launch chain.
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+static int side_stream(SideStream** out) {
+  static SideStream ss[64];
+  int dev = 0;
+  TT_CHECK_HIP(hipGetDevice(&dev));
+  TT_CHECK_ARG(dev >= 0 && dev < 64, "tt_gru_bwd: device %d", dev);
+  SideStream& x = ss[dev];
+  if (!x.s) {
+    TT_CHECK_HIP(hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking));
+    TT_CHECK_HIP(hipEventCreateWithFlags(&x.fork, hipEventDisableTiming));
+    TT_CHECK_HIP(hipEventCreateWithFlags(&x.join, hipEventDisableTiming));
+  }
+  *out = &x;
+  return 0;
+}
 
 extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B, int T, int H, long ldg,
                           long ldy, float drop_p, void* stream) {
@@ -624,12 +658,45 @@ extern "C" int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B
     TT_CHECK_HIP(hipMemsetAsync(r.dbias_part, 0, sizeof(float) * 4L * H * tt_gru_bias_rows(B), st));
   }
   a.B = B; a.T = T; a.H = H; a.ldy = ldy; a.ldd = ldd; a.ldf = ldf;
-  dim3 grid(tt_ceil_div(H, 128) * tt_ceil_div(B, 128) * nrec);
+  if (const char* e = getenv("TT_GRU_DBG")) a.dbg = atoi(e);
+  const int bmr = bwd_rows();
+  // Two independent chains of step launches (recurrences [0, nrec/2) on the caller's
+  // stream, the rest on a side stream): each step kernel is GEMM-then-epilogue, so one
+  // chain's HBM-bound epilogues overlap the other chain's MFMA main loops on the same CUs.
+  const char* e2 = getenv("TT_GRU_BWD_STREAMS");
+  const int ngrp = (nrec >= 2 && !(e2 && atoi(e2) == 1)) ? 2 : 1;
+  BwdArgs ga[2] = {a, a};
+  int gn[2] = {nrec, 0};
+  if (ngrp == 2) {
+    gn[0] = nrec / 2;
+    gn[1] = nrec - gn[0];
+    for (int i = 0; i < gn[1]; ++i) ga[1].r[i] = a.r[gn[0] + i];
+  }
+  hipStream_t gs[2] = {st, st};
+  SideStream* side = nullptr;
+  if (ngrp == 2) {
+    TT_PROPAGATE(side_stream(&side));
+    gs[1] = side->s;
+    TT_CHECK_HIP(hipEventRecord(side->fork, st));
+    TT_CHECK_HIP(hipStreamWaitEvent(side->s, side->fork, 0));
+  }
   for (int s = T - 1; s >= 0; --s) {
-    a.s = s;
-    if (dtype == TT_DT_BF16) hipLaunchKernelGGL(gru_bwd_step<bf16_t>, grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(gru_bwd_step<float>, grid, dim3(256), 0, st, a);
-    TT_CHECK_LAUNCH("gru_bwd_step");
+    for (int g = 0; g < ngrp; ++g) {
+      ga[g].s = s;
+      const dim3 grid(tt_ceil_div(H, 128) * tt_ceil_div(B, bmr) * gn[g]);
+      if (dtype == TT_DT_BF16) {
+        if (bmr == 64) hipLaunchKernelGGL((gru_bwd_step<bf16_t, 64>), grid, dim3(256), 0, gs[g], ga[g]);
+        else hipLaunchKernelGGL((gru_bwd_step<bf16_t, 128>), grid, dim3(256), 0, gs[g], ga[g]);
+      } else {
+        if (bmr == 64) hipLaunchKernelGGL((gru_bwd_step<float, 64>), grid, dim3(256), 0, gs[g], ga[g]);
+        else hipLaunchKernelGGL((gru_bwd_step<float, 128>), grid, dim3(256), 0, gs[g], ga[g]);
+      }
+      TT_CHECK_LAUNCH("gru_bwd_step");
+    }
+  }
+  if (ngrp == 2) {
+    TT_CHECK_HIP(hipEventRecord(side->join, side->s));
+    TT_CHECK_HIP(hipStreamWaitEvent(st, side->join, 0));
   }
   return 0;
 }

@@ -77,6 +77,11 @@ typedef struct {
   void* c[4];
   const float* bias[4];
   int bshift[4];
+  /* a_kouter = 1 only: columns m >= a_split of A come from a_hi[b] + (m - a_split)
+   * (same lda); a_split = 0 disables. Lets dW_hh read the GRU dL/dgh operand, whose
+   * r|z columns live in the dL/dgx buffer, without a copy. */
+  const void* a_hi[4];
+  int a_split;
 } tt_gemm_batch;
 
 int tt_gemm(int dtype, int out_dtype, int a_kouter, int b_kouter, int m, int n, int k,
@@ -124,8 +129,9 @@ typedef struct {
   const void* dy;      /* dL/dy (ldy) or NULL                */
   const float* dfinal; /* dL/dh_final [B, ldf] or NULL       */
   const void* whh;     /* [3H, H]                            */
-  void* dgx;           /* [B*T, ldd]                         */
-  void* dgh;           /* [B*T, ldd]                         */
+  void* dgx;           /* [B*T, ldd]: dL/d(r|z|n pre-activation), 3H columns        */
+  void* dgh;           /* [B*T, ldd]: dL/d(W_hn h + b_hn), H columns; dL/dgh (the
+                          dW_hh operand) is [r|z columns of dgx, this block]        */
   float* dhstate;      /* fp32 scratch [2][B][H] (carry dh*z)  */
   float* dbias_part;   /* fp32 [tt_gru_bias_rows(B)][4H]; zeroed by tt_gru_bwd */
   int dir;

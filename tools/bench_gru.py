@@ -46,8 +46,7 @@ def setup_bwd(B, T, H, keep, dev):
     n = 2
     dY = [torch.randn(B * T, 2 * H, device=dev).to(dt) * 0.01 for _ in range(n)]
     dfin = [torch.randn(B, 2 * H, device=dev) * 0.01 for _ in range(n)]
-    dG = [torch.empty(B * T, 6 * H, device=dev, dtype=dt) for _ in range(n)]
-    dGH = [torch.empty(B * T, 6 * H, device=dev, dtype=dt) for _ in range(n)]
+    dG = [torch.empty(B * T, 8 * H, device=dev, dtype=dt) for _ in range(n)]
     dhs = [torch.empty(2, B, H, device=dev) for _ in range(2 * n)]
     nbr = _lib.load().tt_gru_bias_rows(B)
     part = [torch.empty(nbr, 4 * H, device=dev) for _ in range(2 * n)]
@@ -61,11 +60,11 @@ def setup_bwd(B, T, H, keep, dev):
             r.dfinal = dfin[ti][:, d * H:].data_ptr()
             r.whh = whh[ti][d].data_ptr()
             r.dgx = dG[ti][:, d * 3 * H:].data_ptr()
-            r.dgh = dGH[ti][:, d * 3 * H:].data_ptr()
+            r.dgh = dG[ti][:, 6 * H + d * H:].data_ptr()
             r.dhstate = dhs[ti * 2 + d].data_ptr()
             r.dbias_part = part[ti * 2 + d].data_ptr()
             r.dir = d
-    return recs, (dY, dfin, dG, dGH, dhs, part)
+    return recs, (dY, dfin, dG, dhs, part)
 
 
 def main():
@@ -75,7 +74,7 @@ def main():
     ap.add_argument("--H", type=int, default=512)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--variants", default="seq:0")
-    ap.add_argument("--bwd-variants", default="128:0:1,128:0:2,64:0:2")
+    ap.add_argument("--bwd-variants", default="128:0:2")
     a = ap.parse_args()
     dev = torch.device("cuda")
     recs, keep = setup(a.B, a.T, a.H, dev)
@@ -88,7 +87,7 @@ def main():
         os.environ["TT_GRU_DBG"] = dbg
         os.environ["TT_GRU_BWD_STREAMS"] = strm
         brecs, bkeep = setup_bwd(a.B, a.T, a.H, keep, dev)
-        f = lambda: call("tt_gru_bwd", 1, brecs, 4, a.B, a.T, a.H, 2 * a.H, 6 * a.H, 2 * a.H, st)
+        f = lambda: call("tt_gru_bwd", 1, brecs, 4, a.B, a.T, a.H, 2 * a.H, 8 * a.H, 2 * a.H, st)
         f()
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -30,6 +30,8 @@ class GemmBatch(ctypes.Structure):
         ("c", c_void_p * 4),
         ("bias", c_void_p * 4),
         ("bshift", c_int * 4),
+        ("a_hi", c_void_p * 4),
+        ("a_split", c_int),
     ]
 
 

@@ -29,6 +29,8 @@ struct GemmArgs {
   void* c[4];
   const float* bias[4];
   int bshift[4];
+  const void* a_hi[4];
+  int a_split;
   long lda, ldb, ldc;
   int M, N, K;
   int splits, kt_per_split;
@@ -93,7 +95,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_kernel(GemmArgs g) {
     }
   };
   if constexpr (AKO) {
-    run(ttg::KOPlain<T>{A, g.lda, m0, g.M - m0});
+    ttg::KOPlain<T> la{A, g.lda, m0, g.M - m0};
+    if (g.a_split > 0) {
+      la.base1 = static_cast<const T*>(g.a_hi[bi]);
+      la.csplit = g.a_split;
+    }
+    run(la);
   } else {
     run(ttg::KCPlain<T>{A, g.lda, m0, g.M});
   }
@@ -292,9 +299,15 @@ extern "C" int tt_gemm(int dtype, int out_dtype, int a_kouter, int b_kouter, int
     g.c[b] = batch->c[b];
     g.bias[b] = batch->bias[b];
     g.bshift[b] = batch->bshift[b];
+    g.a_hi[b] = batch->a_hi[b];
+    if (batch->a_split > 0)
+      TT_CHECK_ARG(batch->a_hi[b] && (uintptr_t)batch->a_hi[b] % 16 == 0, "tt_gemm: a_hi[%d] null or misaligned", b);
     if (batch->bshift[b] != 0) shift = true;
   }
   TT_CHECK_ARG(!shift || (b_kouter && seq_t > 0), "tt_gemm: bshift needs b_kouter and seq_t");
+  TT_CHECK_ARG(batch->a_split >= 0 && (batch->a_split == 0 || (a_kouter && batch->a_split % (16 / esz) == 0)),
+               "tt_gemm: a_split %d needs a_kouter and a 16-byte multiple", batch->a_split);
+  g.a_split = batch->a_split;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = m; g.N = n; g.K = k;
   g.alpha = alpha; g.beta = beta_accum; g.relu = relu; g.seq_t = seq_t;

@@ -48,7 +48,7 @@ struct Img {
 
 // ---- loaders -------------------------------------------------------------------
 // A KC loader provides rowptr(r): pointer to element (r, k=0) of tile-row r, or nullptr.
-// A KO loader provides kptr(k): pointer to element (k, tile column 0), or nullptr,
+// A KO loader provides at(k, col): pointer to element (k, tile column col), or nullptr,
 // and ncols: number of valid tile columns (tail).
 
 // First n (< elements per chunk) elements of a 16-byte chunk, zero-filled: the
@@ -84,10 +84,10 @@ TT_DEV void stage_load(const L& ld, int kt, int K, uint4 (&r)[Img<T, KO, ROWS>::
       constexpr int CPR = ROWS * (int)sizeof(T) / 16;  // chunks per k-row
       const int kl = id / CPR, c = id % CPR;
       const int k = kt * (KTB / (int)sizeof(T)) + kl;
-      const T* p = (k < K) ? ld.kptr(k) : nullptr;
       const int col = c * EPC;
-      if (p != nullptr && col < ld.ncols)
-        v = (col + EPC <= ld.ncols) ? *reinterpret_cast<const uint4*>(p + col) : load_partial(p + col, ld.ncols - col);
+      const T* p = (k < K && col < ld.ncols) ? ld.at(k, col) : nullptr;
+      if (p != nullptr)
+        v = (col + EPC <= ld.ncols) ? *reinterpret_cast<const uint4*>(p) : load_partial(p, ld.ncols - col);
     }
     r[i] = v;
   }
@@ -264,8 +264,8 @@ TT_DEV void stage_dma(const L& ld, int kt, int K, char* img) {
       if constexpr (sizeof(T) == 2) c = q ^ (ko_v(kl) << 1);
       else c = q ^ (((kl >> 2) & 1) << 2);
       const int k = kt * (KTB / (int)sizeof(T)) + kl;
-      const T* kp = (k < K) ? ld.kptr(k) : nullptr;
-      if (kp != nullptr && c * EPC < ld.ncols) src = kp + c * EPC;
+      const T* kp = (k < K && c * EPC < ld.ncols) ? ld.at(k, c * EPC) : nullptr;
+      if (kp != nullptr) src = kp;
     }
     __builtin_amdgcn_global_load_lds(src, (lds_void*)(img + i * 1024), 16, 0, 0);
   }
@@ -358,9 +358,9 @@ TT_DEV void stage_dma2(const L& ld, int kt, int K, char* img) {
     if constexpr (!KO) {
       const int row = p >> 3;
       const int c = (p & 7) ^ ((row >> 1) & 7);
-      const T* rp = ld.rowptr(row);
       const int k = kt * (KTB / (int)sizeof(T)) + c * EPC;
-      if (rp != nullptr && k < K) src = rp + k;
+      const T* rp = k < K ? ld.at(row, k) : nullptr;
+      if (rp != nullptr) src = rp;
     } else {
       const int sub = p >> 10, pp = p & 1023;
       constexpr int CPR = 128 * (int)sizeof(T) / 16;
@@ -370,8 +370,8 @@ TT_DEV void stage_dma2(const L& ld, int kt, int K, char* img) {
       else c = q ^ (((kl >> 2) & 1) << 2);
       const int col = sub * 128 + c * EPC;
       const int k = kt * (KTB / (int)sizeof(T)) + kl;
-      const T* kp = (k < K) ? ld.kptr(k) : nullptr;
-      if (kp != nullptr && col < ld.ncols) src = kp + col;
+      const T* kp = (k < K && col < ld.ncols) ? ld.at(k, col) : nullptr;
+      if (kp != nullptr) src = kp;
     }
     dma16(src, base + (uint32_t)i * 1024u);
   }
@@ -491,7 +491,7 @@ struct Loop8 {
         const int col = roff + c * EPC;
         const int k0 = kt0 * KTE + kl;
         if (col < ld.ncols && k0 < K) {
-          pc[j].p = reinterpret_cast<const char*>(ld.base + (long)k0 * ld.ld + ld.c0 + col);
+          pc[j].p = reinterpret_cast<const char*>(ld.raw_at(k0, col));
           pc[j].lim = min(ktl - kt0, (K - k0 + KTE - 1) / KTE);
           if constexpr (L::SHIFTED) pc[j].t0 = k0 % ld.T_;
         }
@@ -604,17 +604,39 @@ TT_DEV int xcd_remap(int bid, int nwg) {
 }
 
 // ---- common loaders ------------------------------------------------------------
+// K-contig loaders: rowptr(r) = row r of the tile at k = 0 (or nullptr past the end);
+// at(r, k) = element (r, k) (or nullptr). K-outer loaders: at(k, col) = element (k, tile
+// column col) (or nullptr), raw_at = the same ignoring any row shift.
 template <typename T>
 struct KCPlain {  // rows [r0, r0+ROWS) of a row-major [rows][ld] matrix
   static constexpr bool SHIFTED = false;
   const T* base; long ld; int r0, rows;
   TT_DEV const T* rowptr(int r) const { int g = r0 + r; return g < rows ? base + (long)g * ld : nullptr; }
+  TT_DEV const T* at(int r, int k) const { const T* p = rowptr(r); return p ? p + k : nullptr; }
+};
+// K-contig operand whose columns [0, ksplit) come from base0 and [ksplit, K) from base1
+// (same rows and ld): the GRU dL/dgh operand, whose r|z columns are shared with dL/dgx.
+template <typename T>
+struct KCSplit {
+  static constexpr bool SHIFTED = false;
+  const T* base0; const T* base1; long ld; int r0, rows, ksplit;
+  TT_DEV const T* at(int r, int k) const {
+    const int g = r0 + r;
+    if (g >= rows) return nullptr;
+    return k < ksplit ? base0 + (long)g * ld + k : base1 + (long)g * ld + (k - ksplit);
+  }
 };
 template <typename T>
 struct KOPlain {  // columns [c0, c0+128) of a row-major [K][ld] matrix
   static constexpr bool SHIFTED = false;
   const T* base; long ld; int c0, ncols;
-  TT_DEV const T* kptr(int k) const { return base + (long)k * ld + c0; }
+  const T* base1 = nullptr;  // columns >= csplit (absolute) come from base1 + (col - csplit)
+  int csplit = 0x7fffffff;
+  TT_DEV const T* raw_at(long k, int col) const {
+    const int gc = c0 + col;
+    return gc < csplit ? base + k * ld + gc : base1 + k * ld + (gc - csplit);
+  }
+  TT_DEV const T* at(long k, int col) const { return raw_at(k, col); }
 };
 // K-outer operand whose k index is (b*T + t) and whose source row is (b*T + t + shift),
 // zero when t+shift falls outside [0,T). Used for the GRU h_{s-1} operand of dW_hh.
@@ -622,11 +644,12 @@ template <typename T>
 struct KOShift {
   static constexpr bool SHIFTED = true;
   const T* base; long ld; int c0, ncols, T_, shift;
-  TT_DEV const T* kptr(int k) const {
-    const int t = k % T_;
+  TT_DEV const T* raw_at(long k, int col) const { return base + k * ld + c0 + col; }
+  TT_DEV const T* at(long k, int col) const {
+    const int t = (int)(k % T_);
     const int ts = t + shift;
     if (ts < 0 || ts >= T_) return nullptr;
-    return base + (long)(k + shift) * ld + c0;
+    return base + (k + shift) * ld + c0 + col;
   }
 };
 

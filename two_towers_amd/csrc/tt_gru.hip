@@ -52,6 +52,7 @@ struct GateRows {
     const int g = rem >> 5, j = j0 + half * 32 + (rem & 31);
     return j < H ? w + (long)(g * H + j) * H : nullptr;
   }
+  TT_DEV const T* at(int r, int k) const { const T* p = rowptr(r); return p ? p + k : nullptr; }
 };
 
 template <typename T>
@@ -180,6 +181,7 @@ __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
   const int tn = R.dir ? t - 1 : t + 1;  // time of step s+1
   const int tp = R.dir ? t + 1 : t - 1;  // time of step s-1
   const bool last = (s == T_ - 1);
+  const T* DGX = static_cast<const T*>(R.dgx);
   const T* DGH = static_cast<const T*>(R.dgh);
 
   f32x4 acc[ML::TM][ML::TN];
@@ -188,7 +190,8 @@ __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
 #pragma unroll
     for (int j = 0; j < ML::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (!last && !(a.dbg & 32)) {
-    ttg::KCPlain<T> la{DGH + (long)tn * a.ldd, (long)T_ * a.ldd, m0, a.B};
+    // dL/dgh_{s+1} = [dL/dar, dL/daz | dL/d(W_hn h)]: r|z from the dgx buffer, n from dgh
+    ttg::KCSplit<T> la{DGX + (long)tn * a.ldd, DGH + (long)tn * a.ldd, (long)T_ * a.ldd, m0, a.B, 2 * H};
     ttg::KOPlain<T> lb{static_cast<const T*>(R.whh), H, j0, H - j0};
     const int K = 3 * H;
     const int nk = (K * (int)sizeof(T) + ttg::KTB - 1) / ttg::KTB;
@@ -208,14 +211,14 @@ __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
   const T* S = static_cast<const T*>(R.save);
   const T* Y = static_cast<const T*>(R.y);
   const T* DY = static_cast<const T*>(R.dy);
-  T* DGX = static_cast<T*>(R.dgx);
+  T* DGXw = static_cast<T*>(R.dgx);
   T* DGHw = static_cast<T*>(R.dgh);
   float* cr_cur = R.dh + (long)cur * a.B * H;        // carry_s = dh_s * z_s
   const float* cr_nxt = R.dh + (long)nxt * a.B * H;  // carry_{s+1}
   const long S4 = 4L * H;
   const int jg = (tid & 15) * 8;
   const int j = j0 + jg;
-  const __amdgpu_buffer_rsrc_t grs = tt_rsrc(DGX + ((long)m0 * T_ + t) * a.ldd);
+  const __amdgpu_buffer_rsrc_t grs = tt_rsrc(DGXw + ((long)m0 * T_ + t) * a.ldd);
   float bsum[4][8];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
@@ -279,15 +282,15 @@ __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
           bsum[0][e] += drp; bsum[1][e] += dzp; bsum[2][e] += dnp; bsum[3][e] += dnp * rg;
         }
         st8(cr_cur + (long)b * H + j, cout);
-        T* gw = DGHw + row * a.ldd + j;
-        // dL/dg is next read by the weight-gradient GEMMs only: stream it past L2
-        const int go = (int)((((long)(b - m0) * T_) * a.ldd + j) * (long)sizeof(T));
-        st8_sc1(grs, go, o_r, (T*)nullptr);
-        st8_sc1(grs, go + H * (int)sizeof(T), o_z, (T*)nullptr);
-        st8_sc1(grs, go + 2 * H * (int)sizeof(T), o_n, (T*)nullptr);
-        st8(gw, o_r);
-        st8(gw + H, o_z);
-        st8(gw + 2 * H, o_hn);
+        // dL/dar, dL/daz are shared by dL/dgx and dL/dgh and re-read by the next step's
+        // GEMM: plain stores. dL/dan is next read by the weight-gradient GEMMs only:
+        // stream it past L2. dL/d(W_hn h) goes to its own H-column block.
+        T* xw = DGXw + row * a.ldd + j;
+        st8(xw, o_r);
+        st8(xw + H, o_z);
+        const int go = (int)((((long)(b - m0) * T_) * a.ldd + j + 2 * H) * (long)sizeof(T));
+        st8_sc1(grs, go, o_n, (T*)nullptr);
+        st8(DGHw + row * a.ldd + j, o_hn);
       }
     }
     __syncthreads();

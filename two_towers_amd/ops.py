@@ -29,8 +29,9 @@ def gemm(a: Sequence[torch.Tensor], b: Sequence[torch.Tensor], c: Sequence[torch
          out_dtype: torch.dtype, bias: Sequence[torch.Tensor | None] | None = None,
          bshift: Sequence[int] | None = None, alpha: float = 1.0, accumulate: bool = False,
          relu: bool = False, seq_t: int = 0, drop_seed: int = 0, drop_p: float = 0.0,
-         splits: int | None = None):
-    """Batched C_i = alpha * op(A_i) op(B_i)^T (+bias) for up to 4 problems of one shape."""
+         splits: int | None = None, a_hi: Sequence[torch.Tensor] | None = None, a_split: int = 0):
+    """Batched C_i = alpha * op(A_i) op(B_i)^T (+bias) for up to 4 problems of one shape.
+    With a_kouter and a_split > 0, A columns >= a_split are read from a_hi[i]."""
     nb = len(a)
     assert 1 <= nb <= 4 and len(b) == nb and len(c) == nb
     bt = GemmBatch()
@@ -42,6 +43,9 @@ def gemm(a: Sequence[torch.Tensor], b: Sequence[torch.Tensor], c: Sequence[torch
         bt.c[i] = c[i].data_ptr()
         bt.bias[i] = bias[i].data_ptr() if bias is not None and bias[i] is not None else None
         bt.bshift[i] = bshift[i] if bshift is not None else 0
+        if a_split:
+            bt.a_hi[i] = a_hi[i].data_ptr()
+    bt.a_split = a_split
     lib = _lib.load()
     if splits is None:
         splits = lib.tt_gemm_pick_splits(m, n, k, nb)

@@ -12,7 +12,8 @@ Layout in HBM (per tower; row = b*T + t, dt = compute dtype):
   G   [B*T, 6H]  dt   input projections, fwd gates r|z|n then rev gates
   Y   [B*T, 2H]  dt   layer output h_t (fwd | rev), X1 = dropout(Y0) (layer-1 input)
   S   [B*T, 4H]  dt   saved pre-activations of r|z|n and gh_n per direction
-  dG, dGH [B*T, 6H] dt  gradients wrt gate pre-activations (input / hidden side)
+  dG  [B*T, 8H]  dt   gradients wrt gate pre-activations: dL/dg_x r|z|n (fwd, rev) in
+                      [0, 6H), dL/d(W_hn h) (fwd, rev) in [6H, 8H); dL/dg_h shares r|z
 """
 from __future__ import annotations
 
@@ -159,12 +160,13 @@ def _gru_layer_fwd(cfg, xs, K, ldx, packs, layer, B, T, seeds, want_x1):
 
 
 def _gru_layer_bwd(cfg, layer, B, T, S, Y, dY, dfinal, packs):
-    """Returns dG, dGH ([B*T, 6H] per tower) and bias grads (dbih, dbhh per tower/dir)."""
+    """Returns dG ([B*T, 8H] per tower: dL/dg_x of both directions in columns [0, 6H),
+    dL/d(W_hn h) of both directions in [6H, 8H); dL/dg_h = [r|z of dL/dg_x, W_hn block])
+    and bias grads (dbih, dbhh per tower/dir)."""
     n, H, dt, dev = cfg.ntowers, cfg.H, cfg.dtype, Y[0].device
     BT = B * T
     lib = _lib.load()
-    dG = [_alloc((BT, 6 * H), dt, dev) for _ in range(n)]
-    dGH = [_alloc((BT, 6 * H), dt, dev) for _ in range(n)]
+    dG = [_alloc((BT, 8 * H), dt, dev) for _ in range(n)]
     dhs = _alloc((n * 2, 2, B, H), torch.float32, dev)
     nbr = lib.tt_gru_bias_rows(B)
     part = _alloc((n * 2, nbr, 4 * H), torch.float32, dev)
@@ -178,50 +180,52 @@ def _gru_layer_bwd(cfg, layer, B, T, S, Y, dY, dfinal, packs):
             r.dfinal = dfinal[ti][:, d * H:].data_ptr() if dfinal is not None else None
             r.whh = packs[ti].whh[layer][d].data_ptr()
             r.dgx = dG[ti][:, d * 3 * H:].data_ptr()
-            r.dgh = dGH[ti][:, d * 3 * H:].data_ptr()
+            r.dgh = dG[ti][:, 6 * H + d * H:].data_ptr()
             r.dhstate = dhs[ti * 2 + d].data_ptr()
             r.dbias_part = part[ti * 2 + d].data_ptr()
             r.dir = d
     ldf = dfinal[0].shape[1] if dfinal is not None else 0
     # algorithmic bytes per (row, unit): saved 4 + h_{s-1} 1 (+ dY 1) + dgh_{s+1} 3 (GEMM
-    # operand) + dgx 3 + dgh 3 elements of dt, plus the fp32 carry read and written (8 B)
+    # operand) + 4 written gradients (r, z, n, W_hn h) of dt, plus the fp32 carry read
+    # and written (8 B)
     esz = 2 if dt == torch.bfloat16 else 4
     with timing.region("gru_bwd_step", T, 2.0 * B * 3 * H * H * 2 * n * (T - 1),
-                       float(B * T * H * 2 * n * (esz * (14 + (1 if dY is not None else 0)) + 8))):
-        call("tt_gru_bwd", dtype_code(dt), recs, 2 * n, B, T, H, 2 * H, 6 * H, ldf, stream_ptr(dev))
+                       float(B * T * H * 2 * n * (esz * (12 + (1 if dY is not None else 0)) + 8))):
+        call("tt_gru_bwd", dtype_code(dt), recs, 2 * n, B, T, H, 2 * H, 8 * H, ldf, stream_ptr(dev))
     sums = _alloc((n * 2, 4 * H), torch.float32, dev)
     for i in range(2 * n):
         ops.colsum(part[i], nbr, 4 * H, 4 * H, sums[i])
     dbih = [[sums[ti * 2 + d, : 3 * H] for d in range(2)] for ti in range(n)]
     dbhh = [[torch.cat([sums[ti * 2 + d, : 2 * H], sums[ti * 2 + d, 3 * H:]]) for d in range(2)] for ti in range(n)]
-    return dG, dGH, dbih, dbhh
+    return dG, dbih, dbhh
 
 
-def _weight_grads(cfg, B, T, dG, dGH, Xin, K, ldx, Y):
+def _weight_grads(cfg, B, T, dG, Xin, K, ldx, Y):
     """dW_ih = dG^T Xin, dW_hh = dGH^T Y_{t-1} for all (tower, dir) in two batched TN GEMMs."""
     n, H, dt, dev = cfg.ntowers, cfg.H, cfg.dtype, dG[0].device
     BT = B * T
     dWih = [[_alloc((3 * H, K), torch.float32, dev) for _ in range(2)] for _ in range(n)]
     dWhh = [[_alloc((3 * H, H), torch.float32, dev) for _ in range(2)] for _ in range(n)]
-    a_ih, b_ih, c_ih, a_hh, b_hh, c_hh, sh = [], [], [], [], [], [], []
+    a_ih, b_ih, c_ih, a_hh, a_hi, b_hh, c_hh, sh = [], [], [], [], [], [], [], []
     for ti in range(n):
         for d in range(2):
             a_ih.append(dG[ti][:, d * 3 * H:])
             b_ih.append(Xin[ti])
             c_ih.append(dWih[ti][d])
-            a_hh.append(dGH[ti][:, d * 3 * H:])
+            a_hh.append(dG[ti][:, d * 3 * H:])
+            a_hi.append(dG[ti][:, 6 * H + d * H:])
             b_hh.append(Y[ti][:, d * H:])
             c_hh.append(dWhh[ti][d])
             sh.append(-1 if d == 0 else 1)
     esz = 2 if dt == torch.bfloat16 else 4
     with timing.region("wgrad_ih", 1, 2.0 * 3 * H * K * BT * 2 * n,
                        float(n * (esz * BT * (6 * H + K) + 2 * 3 * H * K * 4))):
-        ops.gemm(a_ih, b_ih, c_ih, m=3 * H, n=K, k=BT, lda=6 * H, ldb=ldx, ldc=K, a_kouter=True, b_kouter=True,
+        ops.gemm(a_ih, b_ih, c_ih, m=3 * H, n=K, k=BT, lda=8 * H, ldb=ldx, ldc=K, a_kouter=True, b_kouter=True,
                  dtype=dt, out_dtype=torch.float32)
     with timing.region("wgrad_hh", 1, 2.0 * 3 * H * H * BT * 2 * n,
                        float(n * (esz * BT * (6 * H + 2 * H) + 2 * 3 * H * H * 4))):
-        ops.gemm(a_hh, b_hh, c_hh, m=3 * H, n=H, k=BT, lda=6 * H, ldb=2 * H, ldc=H, a_kouter=True, b_kouter=True,
-                 dtype=dt, out_dtype=torch.float32, bshift=sh, seq_t=T)
+        ops.gemm(a_hh, b_hh, c_hh, m=3 * H, n=H, k=BT, lda=8 * H, ldb=2 * H, ldc=H, a_kouter=True, b_kouter=True,
+                 dtype=dt, out_dtype=torch.float32, bshift=sh, seq_t=T, a_hi=a_hi, a_split=2 * H)
     return dWih, dWhh
 
 
@@ -312,27 +316,27 @@ class TowersFn(torch.autograd.Function):
             head_grads.append([dw1, db1, dg, dbeta, dw2, db2])
             dhcat.append(dx)
         # ---- GRU layer 1: dfinal enters at the last processed step of each direction
-        dG1, dGH1, dbih1, dbhh1 = _gru_layer_bwd(cfg, 1, B, T, S1, Y1, None, dhcat, packs)
+        dG1, dbih1, dbhh1 = _gru_layer_bwd(cfg, 1, B, T, S1, Y1, None, dhcat, packs)
         Xl1 = X1 if X1 is not None else Y0
-        dWih1, dWhh1 = _weight_grads(cfg, B, T, dG1, dGH1, Xl1, 2 * H, 2 * H, Y1)
+        dWih1, dWhh1 = _weight_grads(cfg, B, T, dG1, Xl1, 2 * H, 2 * H, Y1)
         # dL/dY0 = (dG1 Wih1) * dropout mask  [B*T, 2H]
         dY0 = [_alloc((B * T, 2 * H), dt, dev) for _ in range(n)]
         esz = 2 if dt == torch.bfloat16 else 4
         with timing.region("dgrad_l1", 1, 2.0 * B * T * 2 * H * 6 * H * n,
                            float(n * esz * (B * T * 6 * H + B * T * 2 * H))):
             if X1 is None:
-                ops.gemm(dG1, [p.wih[1] for p in packs], dY0, m=B * T, n=2 * H, k=6 * H, lda=6 * H, ldb=2 * H,
+                ops.gemm(dG1, [p.wih[1] for p in packs], dY0, m=B * T, n=2 * H, k=6 * H, lda=8 * H, ldb=2 * H,
                          ldc=2 * H, a_kouter=False, b_kouter=True, dtype=dt, out_dtype=dt)
             else:
                 for ti in range(n):
-                    ops.gemm([dG1[ti]], [packs[ti].wih[1]], [dY0[ti]], m=B * T, n=2 * H, k=6 * H, lda=6 * H,
+                    ops.gemm([dG1[ti]], [packs[ti].wih[1]], [dY0[ti]], m=B * T, n=2 * H, k=6 * H, lda=8 * H,
                              ldb=2 * H, ldc=2 * H, a_kouter=False, b_kouter=True, dtype=dt, out_dtype=dt,
                              drop_seed=ctx.seeds[ti], drop_p=cfg.drop_p)
-        del dG1, dGH1
+        del dG1
         # ---- GRU layer 0
-        dG0, dGH0, dbih0, dbhh0 = _gru_layer_bwd(cfg, 0, B, T, S0, Y0, dY0, None, packs)
+        dG0, dbih0, dbhh0 = _gru_layer_bwd(cfg, 0, B, T, S0, Y0, dY0, None, packs)
         del dY0
-        dWih0, dWhh0 = _weight_grads(cfg, B, T, dG0, dGH0, X0, Ep, Ep, Y0)
+        dWih0, dWhh0 = _weight_grads(cfg, B, T, dG0, X0, Ep, Ep, Y0)
         grads = []
         for ti in range(n):
             gl = {}

@@ -121,3 +121,16 @@ def test_oracle_is_not_imported_by_the_product():
                 if isinstance(node, (ast.Import, ast.ImportFrom)):
                     mods = [a.name for a in node.names] if isinstance(node, ast.Import) else [node.module or ""]
                     assert not any(m.startswith("oracle") for m in mods), f
+
+
+def test_split_k_picker_fills_the_chip():
+    """Host-side launch heuristics: a small-M/N, long-K weight gradient (the projection
+    head's dW, 8 or 32 tiles) must be split over K; big problems are not split."""
+    from two_towers_amd import _lib
+    lib = _lib.load()
+    for m, n, k in [(256, 512, 8192), (512, 1024, 8192), (1536, 1024, 524288)]:
+        s = lib.tt_gemm_pick_splits(m, n, k, 1)
+        assert s > 1, (m, n, k, s)
+        assert k // s >= 64 * 8 or s == 1
+    assert lib.tt_gemm_pick_splits(524288, 3072, 1024, 2) == 1
+    assert lib.tt_gru_fwd_launches(1, 64, 512) == 1 and lib.tt_gru_fwd_launches(0, 64, 512) == 64

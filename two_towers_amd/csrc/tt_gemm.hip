@@ -262,7 +262,8 @@ extern "C" int tt_gemm_pick_splits(int m, int n, int k, int nbatch) {
   const int smax = std::max(1, std::min(64, tt_ceil_div(k, 64) / 8));
   int best = 1;
   double best_eff = 0.0;
-  for (int s = (int)std::max<long>(1, target / tiles); s <= std::min<long>(smax, 3 * target / tiles + 1); ++s) {
+  const int s_lo = (int)std::min<long>(smax, std::max<long>(1, target / tiles));
+  for (int s = s_lo; s <= std::min<long>(smax, 3 * target / tiles + 1); ++s) {
     const long w = tiles * s;
     const double eff = (double)w / (256.0 * (double)tt_ceil_div(w, 256));
     if (eff > best_eff + 1e-9) { best_eff = eff; best = s; }

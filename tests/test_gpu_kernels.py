@@ -124,3 +124,26 @@ def test_adam_matches_torch():
         o2.step()
     for a, b in zip(ref, mine):
         assert torch.allclose(a.detach(), b.detach().cpu(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("akout,bkout", [(0, 0), (0, 1), (1, 1)])
+@pytest.mark.parametrize("out", [torch.bfloat16, torch.float32])
+def test_gemm_persistent_tiles(akout, bkout, out):
+    """Shapes with >= 512 256x256 tiles and a short K run the persistent kernel (K-tile
+    stream across tiles): ragged M/N/K tails, bias, relu, two batch entries; compared
+    with fp32 math on the same bf16-rounded operands."""
+    dt = torch.bfloat16
+    m, n, k = 8200, 4104, 136
+    g = torch.Generator().manual_seed(5)
+    As = [torch.randn(m, k, generator=g).to(dt).float() for _ in range(2)]
+    Bs = [torch.randn(n, k, generator=g).to(dt).float() for _ in range(2)]
+    bias = [torch.randn(n, generator=g) for _ in range(2)]
+    Ad = [(a.t().contiguous() if akout else a).to(DEV, dt) for a in As]
+    Bd = [(b.t().contiguous() if bkout else b).to(DEV, dt) for b in Bs]
+    C = [torch.empty(m, n, device=DEV, dtype=out) for _ in range(2)]
+    ops.gemm(Ad, Bd, C, m=m, n=n, k=k, lda=m if akout else k, ldb=n if bkout else k, ldc=n, a_kouter=bool(akout),
+             b_kouter=bool(bkout), dtype=dt, out_dtype=out, bias=[b.to(DEV) for b in bias], relu=True, splits=1)
+    for i in range(2):
+        ref = torch.relu(As[i] @ Bs[i].t() + bias[i])
+        tol = 1e-5 if out == torch.float32 else 8e-3
+        assert rel_err(C[i].float(), ref) < tol, (i, rel_err(C[i].float(), ref))

@@ -46,6 +46,9 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--regstage", default="", help="TT_GEMM_REGSTAGE value (9 = no epilogue, timing only)")
     a = ap.parse_args()
+    if a.regstage:
+        os.environ["TT_GEMM_REGSTAGE"] = a.regstage
     for nm in a.shapes.split(","):
         print(json.dumps(run(nm, a.iters)), flush=True)

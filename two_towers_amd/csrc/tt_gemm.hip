@@ -105,6 +105,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_kernel(GemmArgs g) {
     run(ttg::KCPlain<T>{A, g.lda, m0, g.M});
   }
 
+  if (g.force_regstage == 9) {  // timing diagnostics only: main loop without epilogue
+    if (threadIdx.x == 0 && acc[0][0][0] == 12345.f) static_cast<float*>(g.c[bi])[0] = 1.f;
+    return;
+  }
   // ---- epilogue: stage 64-row slices of the fp32 tile in LDS, then every thread
   // finishes 8 consecutive columns of a row and writes them with 16-byte stores.
   const bool partial = g.splits > 1;
@@ -191,6 +195,205 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_kernel(GemmArgs g) {
   }
 }
 
+// ---- persistent 256x256 GEMM: one workgroup per CU walks tiles w, w+nwg, ... and the
+// 8-phase K-tile stream runs straight across tile boundaries: the last K-tiles of tile
+// i prefetch the first K-tiles of tile i+nwg (their pieces re-resolved on the fly), so
+// tile i's epilogue (32-row LDS passes, separate 32 KiB) runs while tile i+nwg's first
+// half-tiles land. No split-K, no accumulate-into-C (those use gemm_kernel).
+template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO>
+__global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
+  using L8 = ttg::Loop8<T, AKO, BKO>;
+  using Piece = typename L8::Piece;
+  constexpr int STG = 32 * 256 * 4;
+  __shared__ __attribute__((aligned(16))) char lds[L8::LDS_BYTES + STG];
+  float* stg = reinterpret_cast<float*>(lds + L8::LDS_BYTES);
+  const int nwg = gridDim.x;
+  const int w = xcd_remap(blockIdx.x, nwg);
+  if (w >= ntiles) return;
+  const int ntn = (g.N + 255) / 256, ntm = (g.M + 255) / 256;
+  const int nk = (g.K * (int)sizeof(T) + ttg::KTB - 1) / ttg::KTB;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, tid = threadIdx.x;
+  const int wr = wave >> 2, bh = (wave & 3) >> 1, bc = (wave & 1) * 64;
+  const int wm = wr * 128, wn = (wave & 3) * 64;
+  const uint32_t base = __builtin_amdgcn_readfirstlane(ttg::lds_addr_of(lds));
+
+  struct TileId { int bi, m0, n0; };
+  auto decode = [&](int q) {
+    TileId t;
+    t.bi = q / (ntm * ntn);
+    const int tile = q - t.bi * (ntm * ntn);
+    t.m0 = (tile / ntn) * 256;
+    t.n0 = (tile % ntn) * 256;
+    return t;
+  };
+  // A / B loaders of tile q (q >= ntiles: a loader whose pieces are all out of range)
+  auto loader_a = [&](int q) {
+    const TileId t = decode(q < ntiles ? q : 0);
+    const T* A = static_cast<const T*>(g.a[t.bi]);
+    if constexpr (AKO) {
+      ttg::KOPlain<T> la{A, g.lda, t.m0, q < ntiles ? g.M - t.m0 : 0};
+      if (g.a_split > 0) {
+        la.base1 = static_cast<const T*>(g.a_hi[t.bi]);
+        la.csplit = g.a_split;
+      }
+      return la;
+    } else {
+      return ttg::KCPlain<T>{A, g.lda, t.m0, q < ntiles ? g.M : t.m0};
+    }
+  };
+  auto loader_b = [&](int q) {
+    const TileId t = decode(q < ntiles ? q : 0);
+    const T* B = static_cast<const T*>(g.b[t.bi]);
+    if constexpr (!BKO) {
+      return ttg::KCPlain<T>{B, g.ldb, t.n0, q < ntiles ? g.N : t.n0};
+    } else if constexpr (SHIFT) {
+      return ttg::KOShift<T>{B, g.ldb, t.n0, q < ntiles ? g.N - t.n0 : 0, g.seq_t, g.bshift[t.bi]};
+    } else {
+      return ttg::KOPlain<T>{B, g.ldb, t.n0, q < ntiles ? g.N - t.n0 : 0};
+    }
+  };
+  auto la = loader_a(w);
+  auto lb = loader_b(w);
+  Piece pa0[2], pa1[2], pb0[2], pb1[2];
+  L8::template init_half<AKO>(la, 0, nk, g.K, 0, pa0);
+  L8::template init_half<AKO>(la, 0, nk, g.K, 128, pa1);
+  L8::template init_half<BKO>(lb, 0, nk, g.K, 0, pb0);
+  L8::template init_half<BKO>(lb, 0, nk, g.K, 128, pb1);
+  long da = ttg::KTB, db = ttg::KTB;
+  if constexpr (AKO) da = (long)L8::KTE * g.lda * (long)sizeof(T);
+  if constexpr (BKO) db = (long)L8::KTE * g.ldb * (long)sizeof(T);
+  L8::issue_half(la, pa0, 0, da, base);
+  L8::issue_half(la, pa1, 0, da, base + L8::HALF);
+  L8::issue_half(lb, pb0, 0, db, base + 2 * L8::HALF);
+  L8::issue_half(lb, pb1, 0, db, base + 3 * L8::HALF);
+  L8::issue_half(lb, pb0, 1, db, base + L8::SLOT + 2 * L8::HALF);
+  L8::issue_half(lb, pb1, 1, db, base + L8::SLOT + 3 * L8::HALF);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  const bool late = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;  // wave row 1
+  if (late) __builtin_amdgcn_s_barrier();
+
+  int git = 0;  // running K-tile index of the stream (slot parity)
+  int ra_off = 0, rb_off = 0;  // K-tile index of the A / B pieces' tile start in this tile's terms
+  for (int q = w; q < ntiles; q += nwg) {
+    const int qn = q + nwg;
+    const TileId cur_t = decode(q);
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint4 fa[2][4], fb[2][4];
+    for (int r = 0; r < nk; ++r, ++git) {
+      const int cs = git & 1;
+      const uint32_t cur = base + cs * L8::SLOT, nxt = base + (cs ^ 1) * L8::SLOT;
+      const char* ia = lds + cs * L8::SLOT + wr * L8::HALF;
+      const char* ib = lds + cs * L8::SLOT + (2 + bh) * L8::HALF;
+      // the stream's next A K-tile belongs to tile qn once r + 1 == nk
+      if (r + 1 == nk) {
+        la = loader_a(qn);
+        L8::template init_half<AKO>(la, 0, nk, g.K, 0, pa0);
+        L8::template init_half<AKO>(la, 0, nk, g.K, 128, pa1);
+        ra_off = nk;
+      }
+      // P1
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[ks][i] = ttg::frag2<T, AKO>(ia, 16 * i, ks);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[ks][j] = ttg::frag2<T, BKO>(ib, bc + 16 * j, ks);
+      }
+      L8::issue_half(la, pa0, r + 1 - ra_off, da, nxt);
+      L8::quad(0, 0, fa, fb, acc);
+      // P2
+      L8::issue_half(la, pa1, r + 1 - ra_off, da, nxt + L8::HALF);
+      L8::quad(0, 1, fa, fb, acc);
+      // P3: the stream's B K-tile r+2 belongs to tile qn once r + 2 == nk
+      if (r + 2 == nk) {
+        lb = loader_b(qn);
+        L8::template init_half<BKO>(lb, 0, nk, g.K, 0, pb0);
+        L8::template init_half<BKO>(lb, 0, nk, g.K, 128, pb1);
+        rb_off = nk;
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[ks][i] = ttg::frag2<T, AKO>(ia, 64 + 16 * i, ks);
+      L8::issue_half(lb, pb0, r + 2 - rb_off, db, cur + 2 * L8::HALF);
+      L8::quad(1, 1, fa, fb, acc);
+      // P4
+      L8::issue_half(lb, pb1, r + 2 - rb_off, db, cur + 3 * L8::HALF);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      L8::quad(1, 0, fa, fb, acc);
+    }
+    ra_off -= nk;
+    rb_off -= nk;
+    if (!late) __builtin_amdgcn_s_barrier();  // re-align the two wave rows
+
+    // ---- epilogue: 8 passes of 32 rows through the separate staging area
+    TO* C = static_cast<TO*>(g.c[cur_t.bi]);
+    const float* bias = g.bias[cur_t.bi];
+    const int m0 = cur_t.m0, n0 = cur_t.n0;
+    const int cg = (tid & 31) * 8, rlo = tid >> 5;  // 8 columns, rows rlo and rlo + 16
+    float bv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bv[e] = 0.f;
+    if (bias) {
+      if (n0 + cg + 8 <= g.N && g.bias_vec_ok) ld8(bias + n0 + cg, bv);
+      else
+        for (int e = 0; e < 8; ++e)
+          if (n0 + cg + e < g.N) bv[e] = bias[n0 + cg + e];
+    }
+    const __amdgpu_buffer_rsrc_t crs = tt_rsrc(C + (long)m0 * g.ldc + n0);
+    for (int p = 0; p < 8; ++p) {
+      const int i0 = (p * 32 - wm) / 16;  // this wave's accumulator rows in the pass
+      if (p * 32 >= wm && p * 32 < wm + 128) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (i >= i0 && i < i0 + 2)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+              for (int rr = 0; rr < 4; ++rr)
+                stg[(16 * (i - i0) + 4 * (lane >> 4) + rr) * 256 + wn + 16 * j + (lane & 15)] = acc[i][j][rr];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int rl = rlo + 16 * k;
+        const int gm = m0 + p * 32 + rl, gn = n0 + cg;
+        if (gm < g.M && gn < g.N) {
+          float v[8];
+          const float4 x0 = *reinterpret_cast<const float4*>(stg + rl * 256 + cg);
+          const float4 x1 = *reinterpret_cast<const float4*>(stg + rl * 256 + cg + 4);
+          v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float x = v[e] * g.alpha + bv[e];
+            if (g.relu) x = fmaxf(x, 0.f);
+            if (g.drop_thresh) x *= tt_dropout_scale(g.drop_seed, gm, gn + e, g.drop_thresh, g.drop_inv_keep);
+            v[e] = x;
+          }
+          TO* dst = C + (long)gm * g.ldc + gn;
+          if (gn + 8 <= g.N && g.vec_ok) {
+            if (g.stream_out)
+              st8_sc1(crs, (int)(((long)(gm - m0) * g.ldc + (gn - n0)) * (long)sizeof(TO)), v, (TO*)nullptr);
+            else
+              st8(dst, v);
+          } else {
+            for (int e = 0; e < 8 && gn + e < g.N; ++e) Elt<TO>::st(dst + e, v[e]);
+          }
+        }
+      }
+      __builtin_amdgcn_s_barrier();  // staging free for the next pass
+    }
+    if (late && qn < ntiles) __builtin_amdgcn_s_barrier();  // re-stagger for the next tile
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing zero-page DMAs land before exit
+}
+
 // out_b[m][n] = alpha * sum_s part_b[s][m][n] (+ bias[n]) (+ out_b)
 template <typename TO>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* ws, long part_stride, int splits,
@@ -233,11 +436,35 @@ int launch_t(int akout, int bkout, bool shift, const GemmArgs& g, long nwg, hipS
 inline bool use_big(int m, int n, long tiles256) { return m >= 256 && n >= 256 && tiles256 >= 256; }
 
 template <typename T, typename TO>
+int launch_persist(int akout, int bkout, bool shift, const GemmArgs& g, int ntiles, hipStream_t st) {
+  dim3 grid((unsigned)std::min(ntiles, 256)), blk(512);
+#define TT_L(AK, BK, SH) hipLaunchKernelGGL((gemm_persist<T, AK, BK, SH, TO>), grid, blk, 0, st, g, ntiles)
+  if (!akout && !bkout) TT_L(false, false, false);
+  else if (!akout && bkout && !shift) TT_L(false, true, false);
+  else if (!akout && bkout && shift) TT_L(false, true, true);
+  else if (akout && !bkout) TT_L(true, false, false);
+  else if (akout && bkout && !shift) TT_L(true, true, false);
+  else TT_L(true, true, true);
+#undef TT_L
+  TT_CHECK_LAUNCH("gemm_persist");
+  return 0;
+}
+
+template <typename T, typename TO>
 int launch_gemm(int akout, int bkout, bool shift, GemmArgs& g, int nbatch, hipStream_t st) {
   constexpr int EPC = 16 / (int)sizeof(T);
   const bool dma = (akout ? g.M % EPC == 0 : g.K % EPC == 0) && (bkout ? g.N % EPC == 0 : g.K % EPC == 0) &&
                    g.force_regstage != 1;
   const long t256 = (long)tt_ceil_div(g.M, 256) * tt_ceil_div(g.N, 256) * nbatch * g.splits;
+  // persistent tiles with the epilogue under the next tile's first K-tiles: many tiles,
+  // short K (the epilogue is a large share of a tile: measured faster up to 16 K-tiles,
+  // slower at 48 and 128), no split-K, no accumulate (env TT_GEMM_PERSIST=0 disables)
+  static const char* pe = getenv("TT_GEMM_PERSIST");
+  const bool persist_ok = !(pe && pe[0] == '0');
+  const int nk = (g.K * (int)sizeof(T) + ttg::KTB - 1) / ttg::KTB;
+  if (dma && persist_ok && g.force_regstage == 0 && g.splits == 1 && !g.beta && nk >= 2 && nk <= 24 && t256 >= 512 &&
+      use_big(g.M, g.N, t256))
+    return launch_persist<T, TO>(akout, bkout, shift, g, (int)t256, st);
   if (dma && g.force_regstage != 2 && use_big(g.M, g.N, t256))
     return launch_t<T, TO, 256, 256, 2, 4, true>(akout, bkout, shift, g, t256, st);
   const long t128 = (long)tt_ceil_div(g.M, 128) * tt_ceil_div(g.N, 128) * nbatch * g.splits;

@@ -112,6 +112,29 @@ def cpu_baseline(args):
                       f"torch {torch.__version__} CPU, {threads} threads"}
 
 
+# HBM traffic per launch of a timing region, from the committed rocprofv3 PMC summary of
+# this build (tools/pmc_bench.sh: separate FETCH_SIZE / WRITE_SIZE passes over bench.py,
+# hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1 KiB per dispatch, the gfx950 correction of
+# MI355X_MICROARCH.md). A region launch may cover several dispatches (the GRU backward
+# runs two chains of step kernels), hence the dispatches-per-step scaling.
+PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_summary.json")
+REGION_KERNEL = {"gru_bwd_step": "gru_bwd_step<", "gru_fwd": "gru_fwd_seq<", "embed_gather": "embed_gather_kernel"}
+
+
+def pmc_traffic(region, launches_per_step):
+    key = REGION_KERNEL.get(region)
+    if key is None or not os.path.exists(PMC_SUMMARY):
+        return {"traffic": None}
+    with open(PMC_SUMMARY) as f:
+        summ = json.load(f)
+    hits = [v for k, v in summ.items() if key in k and "hbm_bytes_est" in v and "dispatches_per_step" in v]
+    if not hits:
+        return {"traffic": None}
+    per_step = sum(v["hbm_bytes_est"] * v["dispatches_per_step"] for v in hits)
+    return {"traffic": round(per_step / max(launches_per_step, 1)), "traffic_unit": "bytes/launch",
+            "traffic_source": "profiles/r01_pmc_summary.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE)"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -204,7 +227,7 @@ def main():
         return out
 
     dom = max(kt, key=lambda k: kt[k]["ms_total"])
-    roofline = {"kernel": dom, **roof(dom), "traffic": None}
+    roofline = {"kernel": dom, **roof(dom), **pmc_traffic(dom, kt[dom]["launches"] / max(args.steps, 1))}
     extra = {k: roof(k) for k in kt if k != dom}
     step_ms = 1e3 * elapsed / args.steps
     kernels = {k: {"ms_per_step": round(v["ms_total"] / args.steps, 3),

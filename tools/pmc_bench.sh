@@ -14,5 +14,6 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU_M
   timeout -k 10 600 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $OUT/p$i -o p -- \
     python $ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline "$@" > $OUT/p$i.log 2>&1 || { echo "pmc pass $i failed"; exit 1; }
 done
-python $ROOT/tools/pmc_summary.py $OUT > $OUT/summary.json
+# 1 warm-up + 2 timed steps per pass -> dispatches per training step
+python $ROOT/tools/pmc_summary.py $OUT 3 > $OUT/summary.json
 echo pmc done

@@ -1,4 +1,5 @@
-"""Per-kernel mean of every collected counter across rocprofv3 --pmc passes.
+"""Per-kernel mean of every collected counter across rocprofv3 --pmc passes
+(usage: pmc_summary.py DIR [STEPS_TOTAL] -> JSON on stdout).
 FETCH_SIZE / WRITE_SIZE are KB; on gfx950 FETCH_SIZE counts half the bytes of wide
 coalesced reads (MI355X_MICROARCH.md §HBM), so hbm_bytes = 2*FETCH + WRITE (x1024)."""
 import csv
@@ -14,7 +15,7 @@ def short(name):
     return n.split("(")[0][:110]
 
 
-def main(d):
+def main(d, steps_total=None):
     acc = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(d, "p*", "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
@@ -25,6 +26,8 @@ def main(d):
         m["dispatches"] = max(len(v) for v in cs.values())
         if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
             m["hbm_bytes_est"] = (2 * m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024
+        if steps_total:
+            m["dispatches_per_step"] = m["dispatches"] / float(steps_total)
         if "TCC_HIT_sum" in m and "TCC_MISS_sum" in m:
             m["l2_hit_rate"] = m["TCC_HIT_sum"] / max(1.0, m["TCC_HIT_sum"] + m["TCC_MISS_sum"])
         out[k] = m
@@ -32,4 +35,4 @@ def main(d):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else None)

@@ -108,18 +108,39 @@ struct Raw8 {
   }
 };
 
-TT_DEV float tt_sigmoid(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// v_rcp_f32 (1 ulp): a plain 1.0f / x compiles to the ~11-instruction IEEE division
+// sequence, which dominated the GRU epilogues' VALU time.
+TT_DEV float tt_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+TT_DEV float tt_sigmoid(float x) { return tt_rcp(1.0f + __expf(-x)); }
 TT_DEV float tt_tanh(float x) {
   // tanh(x) = 1 - 2/(exp(2x)+1); saturates cleanly for large |x|.
   float e = __expf(2.0f * x);
-  return 1.0f - 2.0f / (e + 1.0f);
+  return 1.0f - 2.0f * tt_rcp(e + 1.0f);
 }
 
 // 1 - tanh(x)^2 without cancellation: 4 e^{-2|x|} / (1 + e^{-2|x|})^2.
 TT_DEV float tt_sech2(float x) {
   const float e = __expf(-2.0f * fabsf(x));
-  const float d = 1.0f + e;
-  return 4.0f * e / (d * d);
+  const float r = tt_rcp(1.0f + e);
+  return 4.0f * e * r * r;
+}
+
+// sigma(x) and sigma(-x) = 1 - sigma(x) from one exp and one reciprocal, without the
+// cancellation of 1 - sigma(x) and without overflow: E = e^{-|x|} in (0, 1].
+TT_DEV void tt_sigmoid_pair(float x, float& s, float& sm) {
+  const float e = __expf(-fabsf(x));
+  const float p = tt_rcp(1.0f + e);  // sigma(|x|)
+  const float q = e * p;                 // sigma(-|x|)
+  s = x >= 0.f ? p : q;
+  sm = x >= 0.f ? q : p;
+}
+// tanh(x) and 1 - tanh(x)^2 from one exp and one reciprocal (E = e^{-2|x|}).
+TT_DEV void tt_tanh_sech2(float x, float& th, float& sech2) {
+  const float e = __expf(-2.0f * fabsf(x));
+  const float r = tt_rcp(1.0f + e);
+  const float t = (1.0f - e) * r;
+  th = x >= 0.f ? t : -t;
+  sech2 = 4.0f * e * r * r;
 }
 
 // Counter-based dropout mask shared by the forward (GRU layer-0 output) and

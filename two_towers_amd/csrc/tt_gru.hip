@@ -271,10 +271,11 @@ __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float dht = Lc[e] + cin[e] + dy[e];
-          const float rg = tt_sigmoid(ar[e]), omr = tt_sigmoid(-ar[e]);
-          const float zg = tt_sigmoid(az[e]), omz = tt_sigmoid(-az[e]);
-          const float ng = tt_tanh(an[e]);
-          const float dnp = dht * omz * tt_sech2(an[e]);
+          float rg, omr, zg, omz, ng, sech2;
+          tt_sigmoid_pair(ar[e], rg, omr);
+          tt_sigmoid_pair(az[e], zg, omz);
+          tt_tanh_sech2(an[e], ng, sech2);
+          const float dnp = dht * omz * sech2;
           const float drp = dnp * gh[e] * rg * omr;
           const float dzp = dht * (hp[e] - ng) * zg * omz;
           o_r[e] = drp; o_z[e] = dzp; o_n[e] = dnp; o_hn[e] = dnp * rg;

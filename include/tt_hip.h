@@ -132,7 +132,7 @@ typedef struct {
   void* dgx;           /* [B*T, ldd]: dL/d(r|z|n pre-activation), 3H columns        */
   void* dgh;           /* [B*T, ldd]: dL/d(W_hn h + b_hn), H columns; dL/dgh (the
                           dW_hh operand) is [r|z columns of dgx, this block]        */
-  float* dhstate;      /* fp32 scratch [2][B][H] (carry dh*z)  */
+  void* dhstate;       /* scratch [2][B][H] of dtype (carry dh*z) */
   float* dbias_part;   /* fp32 [tt_gru_bias_rows(B)][4H]; zeroed by tt_gru_bwd */
   int dir;
 } tt_gru_bwd_rec;

@@ -47,7 +47,7 @@ def setup_bwd(B, T, H, keep, dev):
     dY = [torch.randn(B * T, 2 * H, device=dev).to(dt) * 0.01 for _ in range(n)]
     dfin = [torch.randn(B, 2 * H, device=dev) * 0.01 for _ in range(n)]
     dG = [torch.empty(B * T, 8 * H, device=dev, dtype=dt) for _ in range(n)]
-    dhs = [torch.empty(2, B, H, device=dev) for _ in range(2 * n)]
+    dhs = [torch.empty(2, B, H, device=dev, dtype=dt) for _ in range(2 * n)]
     nbr = _lib.load().tt_gru_bias_rows(B)
     part = [torch.empty(nbr, 4 * H, device=dev) for _ in range(2 * n)]
     recs = (GruBwdRec * (2 * n))()

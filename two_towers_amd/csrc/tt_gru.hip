@@ -33,7 +33,7 @@ struct FwdArgs {
 
 struct BwdRec {
   const void* save; const void* y; const void* dy; const float* dfinal; const void* whh;
-  void* dgx; void* dgh; float* dh; float* dbias; int dir;
+  void* dgx; void* dgh; void* dh; float* dbias; int dir;
 };
 struct BwdArgs {
   BwdRec r[4];
@@ -213,8 +213,10 @@ __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
   const T* DY = static_cast<const T*>(R.dy);
   T* DGXw = static_cast<T*>(R.dgx);
   T* DGHw = static_cast<T*>(R.dgh);
-  float* cr_cur = R.dh + (long)cur * a.B * H;        // carry_s = dh_s * z_s
-  const float* cr_nxt = R.dh + (long)nxt * a.B * H;  // carry_{s+1}
+  // carry_s = dh_s * z_s, stored in the compute dtype: it feeds one step's dh exactly
+  // like the bf16 GEMM operand dL/dgh_{s+1} does (same rounding), at half the bytes
+  T* cr_cur = static_cast<T*>(R.dh) + (long)cur * a.B * H;
+  const T* cr_nxt = static_cast<const T*>(R.dh) + (long)nxt * a.B * H;
   const long S4 = 4L * H;
   const int jg = (tid & 15) * 8;
   const int j = j0 + jg;

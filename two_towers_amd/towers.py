@@ -167,7 +167,7 @@ def _gru_layer_bwd(cfg, layer, B, T, S, Y, dY, dfinal, packs):
     BT = B * T
     lib = _lib.load()
     dG = [_alloc((BT, 8 * H), dt, dev) for _ in range(n)]
-    dhs = _alloc((n * 2, 2, B, H), torch.float32, dev)
+    dhs = _alloc((n * 2, 2, B, H), dt, dev)
     nbr = lib.tt_gru_bias_rows(B)
     part = _alloc((n * 2, nbr, 4 * H), torch.float32, dev)
     recs = (GruBwdRec * (2 * n))()
@@ -186,11 +186,11 @@ def _gru_layer_bwd(cfg, layer, B, T, S, Y, dY, dfinal, packs):
             r.dir = d
     ldf = dfinal[0].shape[1] if dfinal is not None else 0
     # algorithmic bytes per (row, unit): saved 4 + h_{s-1} 1 (+ dY 1) + dgh_{s+1} 3 (GEMM
-    # operand) + 4 written gradients (r, z, n, W_hn h) of dt, plus the fp32 carry read
-    # and written (8 B)
+    # operand) + 4 written gradients (r, z, n, W_hn h) + the carry read and written, all
+    # of dt
     esz = 2 if dt == torch.bfloat16 else 4
     with timing.region("gru_bwd_step", T, 2.0 * B * 3 * H * H * 2 * n * (T - 1),
-                       float(B * T * H * 2 * n * (esz * (12 + (1 if dY is not None else 0)) + 8))):
+                       float(B * T * H * 2 * n * esz * (14 + (1 if dY is not None else 0)))):
         call("tt_gru_bwd", dtype_code(dt), recs, 2 * n, B, T, H, 2 * H, 8 * H, ldf, stream_ptr(dev))
     sums = _alloc((n * 2, 4 * H), torch.float32, dev)
     for i in range(2 * n):

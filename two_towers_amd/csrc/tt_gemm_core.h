@@ -515,6 +515,10 @@ struct Loop8 {
         ok = ok && ts >= 0 && ts < ld.T_;
         off += (long)ld.shift * ld.ld * (long)sizeof(T);
       }
+      if constexpr (L::KSPLIT) {  // K-tiles past the split continue in the second base
+        const int skt = ld.ksplit / KTE;
+        if (r >= skt) off += (long)(ld.base1 - ld.base0) * (long)sizeof(T) - (long)skt * KTB;
+      }
       const char* src = ok ? pc[j].p + off : reinterpret_cast<const char*>(g_tt_zero_page);
       dma16(src, img + (uint32_t)(wave + 8 * j) * 1024u);
     }
@@ -609,7 +613,7 @@ TT_DEV int xcd_remap(int bid, int nwg) {
 // column col) (or nullptr), raw_at = the same ignoring any row shift.
 template <typename T>
 struct KCPlain {  // rows [r0, r0+ROWS) of a row-major [rows][ld] matrix
-  static constexpr bool SHIFTED = false;
+  static constexpr bool SHIFTED = false, KSPLIT = false;
   const T* base; long ld; int r0, rows;
   TT_DEV const T* rowptr(int r) const { int g = r0 + r; return g < rows ? base + (long)g * ld : nullptr; }
   TT_DEV const T* at(int r, int k) const { const T* p = rowptr(r); return p ? p + k : nullptr; }
@@ -617,9 +621,10 @@ struct KCPlain {  // rows [r0, r0+ROWS) of a row-major [rows][ld] matrix
 // K-contig operand whose columns [0, ksplit) come from base0 and [ksplit, K) from base1
 // (same rows and ld): the GRU dL/dgh operand, whose r|z columns are shared with dL/dgx.
 template <typename T>
-struct KCSplit {
-  static constexpr bool SHIFTED = false;
+struct KCSplit {  // ksplit: a multiple of the K-tile for the 8-phase loop
+  static constexpr bool SHIFTED = false, KSPLIT = true;
   const T* base0; const T* base1; long ld; int r0, rows, ksplit;
+  TT_DEV const T* rowptr(int r) const { int g = r0 + r; return g < rows ? base0 + (long)g * ld : nullptr; }
   TT_DEV const T* at(int r, int k) const {
     const int g = r0 + r;
     if (g >= rows) return nullptr;
@@ -628,7 +633,7 @@ struct KCSplit {
 };
 template <typename T>
 struct KOPlain {  // columns [c0, c0+128) of a row-major [K][ld] matrix
-  static constexpr bool SHIFTED = false;
+  static constexpr bool SHIFTED = false, KSPLIT = false;
   const T* base; long ld; int c0, ncols;
   const T* base1 = nullptr;  // columns >= csplit (absolute) come from base1 + (col - csplit)
   int csplit = 0x7fffffff;
@@ -642,7 +647,7 @@ struct KOPlain {  // columns [c0, c0+128) of a row-major [K][ld] matrix
 // zero when t+shift falls outside [0,T). Used for the GRU h_{s-1} operand of dW_hh.
 template <typename T>
 struct KOShift {
-  static constexpr bool SHIFTED = true;
+  static constexpr bool SHIFTED = true, KSPLIT = false;
   const T* base; long ld; int c0, ncols, T_, shift;
   TT_DEV const T* raw_at(long k, int col) const { return base + k * ld + c0 + col; }
   TT_DEV const T* at(long k, int col) const {

@@ -46,6 +46,7 @@ struct BwdArgs {
 // B-tile row r of the forward step -> row (gate*H + j) of Whh [3H, H].
 template <typename T>
 struct GateRows {
+  static constexpr bool SHIFTED = false, KSPLIT = false;
   const T* w; int H, j0;
   TT_DEV const T* rowptr(int r) const {
     const int half = r / 96, rem = r - half * 96;
@@ -322,6 +323,156 @@ __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
     for (int q = 0; q < 4; ++q)
       pb[q * H] += red[(0 * 4 + q) * 128 + tid] + red[(1 * 4 + q) * 128 + tid] + red[(2 * 4 + q) * 128 + tid] +
                    red[(3 * 4 + q) * 128 + tid];
+  }
+}
+
+// ---- backward step on 256x256 tiles (bf16): the recurrent GEMM on the 8-phase loop --
+// One workgroup (8 waves) per 256 rows x 256 hidden units of a recurrence: at B 8192,
+// H 512 the four recurrences are exactly 256 tiles, one per CU, so the GEMM runs at the
+// 8-phase loop's rate (the 128x128 two-phase loop reached ~680 TFLOP/s here) and the
+// epilogue (two 128-row passes staged in the freed DMA slots) streams the gate
+// gradients. Bias partials land in partial row 2*mt (tt_gru_bias_rows() counts 128-row
+// tiles; the odd rows stay zero).
+__global__ __launch_bounds__(512) void gru_bwd_big(BwdArgs a) {
+  using L8 = ttg::Loop8<bf16_t, false, true>;
+  static_assert(L8::LDS_BYTES >= 128 * 256 * 4 && L8::LDS_BYTES >= 8 * 4 * 256 * 4, "staging fits the slots");
+  __shared__ __attribute__((aligned(16))) char lds[L8::LDS_BYTES];
+  const int H = a.H, T_ = a.T, s = a.s;
+  const int ntj = (H + 255) / 256, ntm = (a.B + 255) / 256;
+  const int id = ttg::xcd_remap(blockIdx.x, gridDim.x);
+  const int rz = id / (ntm * ntj), rem = id - rz * ntm * ntj;
+  const int mt = rem / ntj;
+  const BwdRec R = a.r[rz];
+  const int m0 = mt * 256, j0 = (rem % ntj) * 256;
+  const int t = R.dir ? T_ - 1 - s : s;
+  const int tn = R.dir ? t - 1 : t + 1;
+  const int tp = R.dir ? t + 1 : t - 1;
+  const bool last = (s == T_ - 1);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, tid = threadIdx.x;
+  const int wm = (wave >> 2) * 128, wn = (wave & 3) * 64;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (!last) {
+    const bf16_t* DGX = static_cast<const bf16_t*>(R.dgx);
+    const bf16_t* DGH = static_cast<const bf16_t*>(R.dgh);
+    ttg::KCSplit<bf16_t> la{DGX + (long)tn * a.ldd, DGH + (long)tn * a.ldd, (long)T_ * a.ldd, m0, a.B, 2 * H};
+    ttg::KOPlain<bf16_t> lb{static_cast<const bf16_t*>(R.whh), H, j0, H - j0};
+    L8::run(la, lb, 3 * H, 0, (3 * H + L8::KTE - 1) / L8::KTE, lds, acc);
+  }
+
+  // ---- epilogue in two passes: pass p stages rows 64p..64p+63 of both wave rows
+  // (tile rows 64p.. and 128+64p..) as an fp32 [128][256] image over the freed slots, so
+  // half of every wave's accumulators die before the gate arithmetic of the first pass.
+  float* L = reinterpret_cast<float*>(lds);
+  const int cur = s & 1, nxt = cur ^ 1;
+  const bf16_t* S = static_cast<const bf16_t*>(R.save);
+  const bf16_t* Y = static_cast<const bf16_t*>(R.y);
+  const bf16_t* DY = static_cast<const bf16_t*>(R.dy);
+  bf16_t* DGXw = static_cast<bf16_t*>(R.dgx);
+  bf16_t* DGHw = static_cast<bf16_t*>(R.dgh);
+  bf16_t* cr_cur = static_cast<bf16_t*>(R.dh) + (long)cur * a.B * H;
+  const bf16_t* cr_nxt = static_cast<const bf16_t*>(R.dh) + (long)nxt * a.B * H;
+  const long S4 = 4L * H;
+  const int jg = (tid & 31) * 8;
+  const int j = j0 + jg;
+  const __amdgpu_buffer_rsrc_t grs = tt_rsrc(DGXw + ((long)m0 * T_ + t) * a.ldd);
+  float bsum[4][8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bsum[q][e] = 0.f;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          L[((wave >> 2) * 64 + 16 * i + 4 * (lane >> 4) + r) * 256 + wn + 16 * jt + (lane & 15)] = acc[4 * p + i][jt][r];
+    __syncthreads();
+#pragma unroll 2
+    for (int k = 0; k < 8; ++k) {
+      const int rl = (tid >> 5) + 16 * k;  // image row: wave row (rl >> 6), row in pass (rl & 63)
+      const int b = m0 + (rl >> 6) * 128 + p * 64 + (rl & 63);
+      if (b < a.B && j < H) {
+        const long row = (long)b * T_ + t;
+        float cin[8], dy[8], ar[8], az[8], an[8], gh[8], hp[8];
+        if (!last) ld8(cr_nxt + (long)b * H + j, cin);
+        else if (R.dfinal) ld8(R.dfinal + (long)b * a.ldf + j, cin);
+        else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cin[e] = 0.f;
+        }
+        if (DY) ld8(DY + row * a.ldy + j, dy);
+        else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dy[e] = 0.f;
+        }
+        const bf16_t* sp = S + row * S4 + j;
+        ld8(sp, ar);
+        ld8(sp + H, az);
+        ld8(sp + 2 * H, an);
+        ld8(sp + 3 * H, gh);
+        if (s > 0) ld8(Y + ((long)b * T_ + tp) * a.ldy + j, hp);
+        else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) hp[e] = 0.f;
+        }
+        const float* Lc = L + rl * 256 + jg;
+        float o_r[8], o_z[8], o_n[8], o_hn[8], cout[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float dht = Lc[e] + cin[e] + dy[e];
+          float rg, omr, zg, omz, ng, sech2;
+          tt_sigmoid_pair(ar[e], rg, omr);
+          tt_sigmoid_pair(az[e], zg, omz);
+          tt_tanh_sech2(an[e], ng, sech2);
+          const float dnp = dht * omz * sech2;
+          const float drp = dnp * gh[e] * rg * omr;
+          const float dzp = dht * (hp[e] - ng) * zg * omz;
+          o_r[e] = drp; o_z[e] = dzp; o_n[e] = dnp; o_hn[e] = dnp * rg;
+          cout[e] = dht * zg;
+          bsum[0][e] += drp; bsum[1][e] += dzp; bsum[2][e] += dnp; bsum[3][e] += dnp * rg;
+        }
+        st8(cr_cur + (long)b * H + j, cout);
+        bf16_t* xw = DGXw + row * a.ldd + j;
+        st8(xw, o_r);
+        st8(xw + H, o_z);
+        const int go = (int)((((long)(b - m0) * T_) * a.ldd + j + 2 * H) * 2L);
+        st8_sc1(grs, go, o_n, (bf16_t*)nullptr);
+        st8(DGHw + row * a.ldd + j, o_hn);
+      }
+    }
+    __syncthreads();
+  }
+  // bias partials of the 256-row tile (all into partial row 2*mt; row 2*mt+1 stays zero):
+  // lanes l and l^32 share columns
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bsum[q][e] += __shfl_xor(bsum[q][e], 32, 64);
+  float* red = L;  // [8 waves][4][256]
+  if (lane < 32) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[(wave * 4 + q) * 256 + lane * 8 + e] = bsum[q][e];
+  }
+  __syncthreads();
+  if (tid < 256 && j0 + tid < H) {
+    float* pb = R.dbias + (long)(mt * 2) * (4L * H) + j0 + tid;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) v += red[(w * 4 + q) * 256 + tid];
+      pb[q * H] += v;
+    }
   }
 }
 
@@ -666,6 +817,18 @@ extern "C" int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B
   a.B = B; a.T = T; a.H = H; a.ldy = ldy; a.ldd = ldd; a.ldf = ldf;
   if (const char* e = getenv("TT_GRU_DBG")) a.dbg = atoi(e);
   const int bmr = bwd_rows();
+  // bf16 with H a multiple of 256: 256x256 tiles on the 8-phase loop, one launch per step
+  // (env TT_GRU_BWD_BIG=0 selects the 128x128 step kernels)
+  const char* e5 = getenv("TT_GRU_BWD_BIG");
+  if (dtype == TT_DT_BF16 && H % 256 == 0 && bmr == 128 && !(e5 && e5[0] == '0')) {
+    const dim3 grid((H / 256) * tt_ceil_div(B, 256) * nrec);
+    for (int s = T - 1; s >= 0; --s) {
+      a.s = s;
+      hipLaunchKernelGGL(gru_bwd_big, grid, dim3(512), 0, st, a);
+      TT_CHECK_LAUNCH("gru_bwd_big");
+    }
+    return 0;
+  }
   // Two independent chains of step launches (recurrences [0, nrec/2) on the caller's
   // stream, the rest on a side stream): each step kernel is GEMM-then-epilogue, so one
   // chain's HBM-bound epilogues overlap the other chain's MFMA main loops on the same CUs.

@@ -118,7 +118,8 @@ def cpu_baseline(args):
 # MI355X_MICROARCH.md). A region launch may cover several dispatches (the GRU backward
 # runs two chains of step kernels), hence the dispatches-per-step scaling.
 PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_summary.json")
-REGION_KERNEL = {"gru_bwd_step": "gru_bwd_step<", "gru_fwd": "gru_fwd_seq<", "embed_gather": "embed_gather_kernel"}
+REGION_KERNEL = {"gru_bwd_step": ("gru_bwd_step<", "gru_bwd_big"), "gru_fwd": ("gru_fwd_seq<",),
+                 "embed_gather": ("embed_gather_kernel",)}
 
 
 def pmc_traffic(region, launches_per_step):
@@ -127,7 +128,8 @@ def pmc_traffic(region, launches_per_step):
         return {"traffic": None}
     with open(PMC_SUMMARY) as f:
         summ = json.load(f)
-    hits = [v for k, v in summ.items() if key in k and "hbm_bytes_est" in v and "dispatches_per_step" in v]
+    hits = [v for k, v in summ.items()
+            if any(s in k for s in key) and "hbm_bytes_est" in v and "dispatches_per_step" in v]
     if not hits:
         return {"traffic": None}
     per_step = sum(v["hbm_bytes_est"] * v["dispatches_per_step"] for v in hits)

@@ -98,7 +98,8 @@ int tt_gemm_pick_splits(int m, int n, int k, int nbatch);
  * n = tanh(Win x + bin + r*(Whn h + bhn)), h' = (1-z) n + z h, h0 = 0).
  * Replaces nn.GRU at enhanced_two_tower.py:51,57 (per layer, up to 4 recurrences =
  * {query,doc} x {fwd,rev} per launch). The input projection g = x Wih^T + bih
- * (+ [bhr, bhz, 0]) is a tt_gemm done by the caller. */
+ * (+ [bhr, bhz, 0]) is a tt_gemm done by the caller. H must be a multiple of 8 (the
+ * epilogues update 8 consecutive hidden units per thread; tt_gru_bwd likewise). */
 typedef struct {
   const void* g;       /* [B*T, ldg]: gate pre-activations r|z|n (3H columns)        */
   const void* whh;     /* [3H, H]                                                    */
@@ -172,6 +173,37 @@ int tt_proj_head_bwd(int dtype, const tt_head_bwd_io* io, int ntower, int B, int
                      void* stream);
 long tt_proj_head_bwd_ws_size(int dtype, int B, int h);
 
+/* Margin-model head Linear(2H->H) -> LayerNorm(H, eps) -> ReLU -> Dropout(drop_p), one
+ * set of weights shared by both towers (margin_two_tower.py:30-35, applied in encode
+ * :58-62). Query and doc rows are stacked into one [rows, 2H] batch, so the weight
+ * gradients of the backward are already the sum over the two towers. C = H. The dropout
+ * mask is the counter-based keep(drop_seed, row, col) of tt_gru_fwd, recomputed by the
+ * backward. Weights in dtype (w1 [C, 2C]); biases/LN affine fp32. */
+typedef struct {
+  const void* x;   /* [rows, 2C] dtype : cat(h_fwd_final, h_rev_final)           */
+  const void* w1; const float* b1; const float* ln_g; const float* ln_b;
+  void* p1;        /* [rows, C] dtype : saved pre-LayerNorm activations          */
+  float* mean;     /* [rows]                                                     */
+  float* rstd;     /* [rows]                                                     */
+  float* out;      /* [rows, C] fp32                                             */
+} tt_head1_fwd_io;
+
+int tt_proj_head1_fwd(int dtype, const tt_head1_fwd_io* io, long rows, int C, float ln_eps, float drop_p,
+                      uint32_t drop_seed, void* stream);
+
+typedef struct {
+  const void* x; const void* w1; const float* ln_g; const float* ln_b;
+  const void* p1; const float* mean; const float* rstd;
+  const float* dout;  /* [rows, C] fp32 upstream gradient                          */
+  float* dx;          /* [rows, 2C] fp32 gradient wrt x                            */
+  float* dw1; float* db1; float* dg; float* dbeta;  /* fp32 grads (overwritten)    */
+  void* ws;           /* scratch, tt_proj_head1_bwd_ws_size bytes                  */
+} tt_head1_bwd_io;
+
+int tt_proj_head1_bwd(int dtype, const tt_head1_bwd_io* io, long rows, int C, float drop_p, uint32_t drop_seed,
+                      void* stream);
+long tt_proj_head1_bwd_ws_size(int dtype, long rows, int C);
+
 /* ---------------------------------------------------------------------- losses */
 /* y = x / max(||x||_2, eps) row-wise (F.normalize, enhanced_two_tower.py:74-75; also
  * the normalisation inside F.cosine_similarity, :112-117,125-128). y in dtype, y32
@@ -202,8 +234,10 @@ long tt_infonce_bwd_ws_size(int dtype, long bq, long nd, int h);
 
 /* Hard-negative mining, batched over rows (get_hard_negatives,
  * enhanced_two_tower.py:123-133): sims = qn dn^T (cosine for normalised inputs), the
- * positive column label_offset+i set to -1 (label_offset < 0: no column masked), top-k (k <= 16) indices per row sorted by
- * descending similarity; ties broken towards the lower column index.
+ * positive column label_offset+i set to -1 (label_offset < 0: no column masked), top-k
+ * (1 <= k <= min(16, nd)) indices per row sorted by descending similarity; ties broken
+ * towards the lower column index. Also the scoring step of the serving /search
+ * (server/python-api/app.py:94-101, label_offset < 0).
  * idx [bq, k] int32, val [bq, k] fp32 (optional). ws: tt_hardneg_ws_size bytes. */
 int tt_hardneg_topk(int dtype, const void* qn, long bq, const void* dn, long nd, int h,
                     long label_offset, int k, int32_t* idx, float* val, void* ws, void* stream);

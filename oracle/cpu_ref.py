@@ -12,6 +12,9 @@ A from-scratch restatement, in plain PyTorch-CPU with explicit GRU cell arithmet
   - get_hard_negatives               enhanced_two_tower.py:123-133
   - EnhancedDataset.text_to_embedding enhanced_two_tower.py:144-166
   - the train_enhanced.py inner loop  train_enhanced.py:54-69 (Adam defaults)
+  - margin TwoTowerModel              margin_two_tower.py:9-68 (shared projection head,
+                                      compute_similarity), its InfoNCE :70-85 and
+                                      SimpleDataset.text_to_embedding :96-153
   - MRR@10 of validate_enhanced.py    validate_enhanced.py:73-80,104-110
 Pinned against golden vectors produced by running the reference itself
 (oracle/gen_goldens.py -> tests/golden/*.npz; checked by tests/test_oracle_golden.py).
@@ -129,6 +132,96 @@ def encode(x: torch.Tensor, p: dict, tower: str, drop_p: float = 0.0, seed: int 
 def forward(q: torch.Tensor, d: torch.Tensor, p: dict, drop_p: float = 0.0, seeds=(0, 0)):
     """EnhancedTwoTowerModel.forward (enhanced_two_tower.py:62-65)."""
     return encode(q, p, "query", drop_p, seeds[0]), encode(d, p, "doc", drop_p, seeds[1])
+
+# ------------------------------------------------------------- margin family
+
+def margin_head(v: torch.Tensor, p: dict, drop_p: float = 0.0, seed: int = 0, row0: int = 0):
+    """projection = Linear(2H,H) -> LayerNorm(H) -> ReLU -> Dropout (margin_two_tower.py:
+    30-35), one set of weights for both towers. Dropout rows are counted from row0 in the
+    query-then-doc stacking the HIP path uses."""
+    a = v @ p["projection.0.weight"].t() + p["projection.0.bias"]
+    a = F.layer_norm(a, (a.shape[1],), p["projection.1.weight"], p["projection.1.bias"], 1e-5)
+    a = torch.relu(a)
+    if drop_p > 0.0:
+        m = dropout_mask(seed, row0 + a.shape[0], a.shape[1], drop_p)[row0:]
+        a = a * torch.from_numpy(m).to(a.dtype)
+    return a
+
+
+def margin_encode(x: torch.Tensor, p: dict, tower: str, drop_p: float = 0.0, seed: int = 0):
+    """TwoTowerModel.encode (margin_two_tower.py:58-62): cat(hidden[-2], hidden[-1])."""
+    enc = "query_encoder" if tower == "query" else "doc_encoder"
+    hn, _ = gru_encoder(x, p, enc, drop_p, seed)
+    return margin_head(torch.cat([hn[-2], hn[-1]], 1), p)
+
+
+def margin_forward(q: torch.Tensor, d: torch.Tensor, p: dict, training: bool):
+    """TwoTowerModel.forward + compute_similarity (margin_two_tower.py:37-48, 64-68),
+    dropout off: (normalize(q), normalize(d)) in training, qn dnᵀ in eval."""
+    qn = normalize(margin_encode(q, p, "query"))
+    dn = normalize(margin_encode(d, p, "doc"))
+    return (qn, dn) if training else qn @ dn.t()
+
+
+def margin_param_shapes(E: int, H: int):
+    """state_dict layout of margin TwoTowerModel(E, H) (margin_two_tower.py:10-35)."""
+    shapes = {}
+    for enc in ("query_encoder", "doc_encoder"):
+        for layer in range(2):
+            inp = E if layer == 0 else 2 * H
+            for sfx in ("", "_reverse"):
+                shapes[f"{enc}.weight_ih_l{layer}{sfx}"] = (3 * H, inp)
+                shapes[f"{enc}.weight_hh_l{layer}{sfx}"] = (3 * H, H)
+                shapes[f"{enc}.bias_ih_l{layer}{sfx}"] = (3 * H,)
+                shapes[f"{enc}.bias_hh_l{layer}{sfx}"] = (3 * H,)
+    shapes["projection.0.weight"] = (H, 2 * H)
+    shapes["projection.0.bias"] = (H,)
+    shapes["projection.1.weight"] = (H,)
+    shapes["projection.1.bias"] = (H,)
+    return shapes
+
+
+_MARGIN_RULES = (
+    (r"\b(is|are|refers?\s+to)\s+(?:a|an|the)\b", "IS"),
+    (r"\b(contains?|has|have|includes?)\b", "HAS"),
+    (r"\b(part|component|element)\s+of\b", "PART_OF"),
+    (r"\b(controls?|regulates?|manages?)\b", "CONTROLS"),
+    (r"\b(functions?|works?|operates?)\b", "FUNCTIONS"),
+    (r"(\d+(?:\.\d+)?)\s*([a-zA-Z]+)", r"\1_\2"),
+)
+
+
+def margin_text_to_ids(text: str, vocab: dict, max_length: int = 30):
+    """SimpleDataset.text_to_embedding (margin_two_tower.py:96-153) as row ids: each rule
+    is applied to the lower-cased result of the previous one; for processed word i the
+    lookups are original word i, then processed word i when it differs; OOV lookups are
+    skipped; one zero row if nothing was found; pad/truncate to max_length."""
+    import re
+    orig = text.lower().split()
+    t = text
+    for pat, rep in _MARGIN_RULES:
+        t = re.sub(pat, rep, t.lower())
+    ids = []
+    for i, w in enumerate(t.split()):
+        cands = ([orig[i]] if i < len(orig) else []) + ([w] if w != orig[i] else [])
+        ids.extend(vocab[c] for c in cands if c in vocab)
+    if not ids:
+        ids = [-1]
+    ids = ids[:max_length]
+    return ids + [-1] * (max_length - len(ids))
+
+def search_results(query_vec, doc_mat, docs, ground_truth, top_k=3):
+    """The /search response body (server/python-api/app.py:94-115) for one encoded query:
+    F.cosine_similarity against every cached row, top_k (ties: lower index first),
+    text = first 200 chars + '...' when longer, is_ground_truth by text equality."""
+    sims = F.cosine_similarity(query_vec.reshape(1, 1, -1), doc_mat.unsqueeze(0), dim=-1).reshape(-1)
+    order = sorted(range(sims.shape[0]), key=lambda j: (-float(sims[j]), j))[:top_k]
+    out = []
+    for r, j in enumerate(order):
+        text = docs[j][:200] + "..." if len(docs[j]) > 200 else docs[j]
+        out.append({"text": text, "score": float(sims[j]), "is_ground_truth": docs[j] in ground_truth,
+                    "rank": r + 1})
+    return out
 
 # ---------------------------------------------------------------------- losses
 

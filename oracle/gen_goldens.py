@@ -251,10 +251,73 @@ def gen_dp(et):
     np.savez_compressed(os.path.join(OUT, "dp_equiv.npz"), **out)
 
 
+def import_margin_reference():
+    sys.path.insert(0, REF)
+    import margin_two_tower as mt  # noqa: E402  (torch / numpy / re only)
+    return mt
+
+
+def gen_margin(mt):
+    """margin_two_tower.TwoTowerModel: eval similarity matrix + encode_* outputs, and one
+    train-mode InfoNCE(0.1) backward (train_margin.py) with every dropout set to 0."""
+    torch.manual_seed(4)
+    model = mt.TwoTowerModel(16, 8).eval()
+    g = torch.Generator().manual_seed(17)
+    q = torch.randn(12, 7, 16, generator=g)
+    d = torch.randn(12, 7, 16, generator=g)
+    with torch.no_grad():
+        sim = model(q, d)
+        eq = model.encode_query(q)
+        ed = model.encode_doc(d)
+    out = {"q": q.numpy(), "d": d.numpy(), "sim": sim.numpy(), "enc_q": eq.numpy(), "enc_d": ed.numpy()}
+    out.update(sd_arrays("w.", model.state_dict()))
+    model.train()
+    model.query_encoder.dropout = 0.0
+    model.doc_encoder.dropout = 0.0
+    model.projection[3].p = 0.0
+    qn, dn = model(q, d)
+    loss = mt.InfoNCELoss(temperature=0.1)(qn, dn)
+    loss.backward()
+    out["qn"] = qn.detach().numpy()
+    out["dn"] = dn.detach().numpy()
+    out["loss"] = np.float32(loss.item())
+    out.update({f"g.{k}": p.grad.numpy() for k, p in model.named_parameters()})
+    np.savez_compressed(os.path.join(OUT, "margin_tiny.npz"), **out)
+
+    # SimpleDataset.text_to_embedding: the marker rewrites and the original/processed
+    # lookup order, with a vocabulary holding both original and rewritten tokens
+    rng = np.random.default_rng(18)
+    words = ["the", "heart", "is", "a", "muscle", "has", "contains", "4_chambers", "4", "chambers", "5_kg",
+             "part_of", "brain", "controls", "functions", "cell", "an", "organ", "works", "3.5_mg", "dose",
+             "refers", "to", "component", "of", "body", "are", "have", "includes", "element", "system"]
+    vecs = rng.standard_normal((len(words), 6)).astype(np.float32)
+    w2v = FakeW2V(words, vecs)
+    texts = [
+        "The heart is a muscle that contains 4 chambers",
+        "the brain controls the body and works as an organ",
+        "Dose: 3.5 mg or 5kg; 4chambers",
+        "a cell is part of the body and refers to an element of a system",
+        "Functions FUNCTION works worked operates",
+        "heart\tmuscle\nbrain",
+        "zzz qqq",
+        "",
+        "the " * 40,
+    ]
+    embs = np.stack([mt.SimpleDataset.text_to_embedding(t, w2v, 10).numpy() for t in texts])
+    np.savez_compressed(os.path.join(OUT, "margin_featurize.npz"), words=np.array(words), vecs=vecs,
+                        texts=np.array(texts), max_length=np.int32(10), emb=embs)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
-    et = import_reference()
     torch.set_num_threads(8)
+    only = set(sys.argv[1:])
+    if only:  # e.g. `gen_goldens.py margin` regenerates just those fixtures
+        if "margin" in only:
+            gen_margin(import_margin_reference())
+        return
+    et = import_reference()
+    gen_margin(import_margin_reference())
     gen_tiny_model(et)
     gen_tiny_train(et)
     gen_featurize(et)

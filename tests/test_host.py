@@ -134,3 +134,80 @@ def test_split_k_picker_fills_the_chip():
         assert k // s >= 64 * 8 or s == 1
     assert lib.tt_gemm_pick_splits(524288, 3072, 1024, 2) == 1
     assert lib.tt_gru_fwd_launches(1, 64, 512) == 1 and lib.tt_gru_fwd_launches(0, 64, 512) == 64
+
+
+def test_margin_dataset_matches_reference_fixture():
+    """two_towers_amd.margin.SimpleDataset / margin_ids vs margin_two_tower.SimpleDataset
+    (tests/golden/margin_featurize.npz, made by oracle/gen_goldens.py)."""
+    import numpy as np
+
+    from two_towers_amd.margin import SimpleDataset, margin_ids
+    from two_towers_amd.data import Vocab
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "margin_featurize.npz"), allow_pickle=False)
+    words = [str(w) for w in z["words"]]
+    vocab = Vocab(words, z["vecs"])
+    T = int(z["max_length"])
+    for text, emb in zip(z["texts"], z["emb"]):
+        text = str(text)
+        np.testing.assert_array_equal(SimpleDataset.text_to_embedding(text, vocab, T).numpy(), emb)
+        ids = margin_ids(text, vocab, T)
+        rows = np.stack([z["vecs"][i] if i >= 0 else np.zeros(z["vecs"].shape[1], np.float32) for i in ids])
+        np.testing.assert_array_equal(rows, emb)
+
+
+def test_margin_model_state_dict_matches_reference_layout():
+    import torch
+
+    from oracle import cpu_ref
+    from two_towers_amd.margin import TwoTowerModel
+    m = TwoTowerModel(300, 512)
+    sd = m.state_dict()
+    shapes = cpu_ref.margin_param_shapes(300, 512)
+    assert {k: tuple(v.shape) for k, v in sd.items()} == shapes
+    torch.manual_seed(0)
+    a = TwoTowerModel(16, 8).state_dict()
+    torch.manual_seed(0)
+    b = TwoTowerModel(16, 8).state_dict()
+    assert all(torch.equal(a[k], b[k]) for k in a)
+
+
+def test_search_response_formatting():
+    """serving.format_results / snippet / query_to_docs_map restate app.py:30-36,104-115."""
+    from two_towers_amd.serving import format_results, query_to_docs_map, snippet
+    long = "x" * 250
+    assert snippet(long) == "x" * 200 + "..." and snippet("short") == "short" and snippet("y" * 200) == "y" * 200
+    docs = ["alpha doc", long, "gamma", "alpha doc"]
+    m = query_to_docs_map(["q1", "q2", "q1"], ["alpha doc", "gamma", long])
+    assert m == {"q1": ["alpha doc", long], "q2": ["gamma"]}
+    res = format_results(docs, m["q1"], [1, 2, 3], [0.9, 0.5, 0.25])
+    assert res == [{"text": "x" * 200 + "...", "score": 0.9, "is_ground_truth": True, "rank": 1},
+                   {"text": "gamma", "score": 0.5, "is_ground_truth": False, "rank": 2},
+                   {"text": "alpha doc", "score": 0.25, "is_ground_truth": True, "rank": 3}]
+    # the oracle's restatement agrees on the same ranking
+    q = torch.tensor([1.0, 0.0])
+    mat = torch.tensor([[0.1, 1.0], [1.0, 0.1], [1.0, 1.0], [-1.0, 0.0]])
+    ref = cpu_ref.search_results(q, mat, docs, m["q1"], 3)
+    assert [r["rank"] for r in ref] == [1, 2, 3] and [r["text"] for r in ref] == ["x" * 200 + "...", "gamma",
+                                                                                  "alpha doc"]
+
+
+def test_search_http_contract():
+    """make_app: POST /search request/response models of app.py:72-123, 500 on errors."""
+    from fastapi.testclient import TestClient
+
+    from two_towers_amd.serving import make_app
+
+    class FakeIndex:
+        def search(self, query):
+            if query == "boom":
+                raise RuntimeError("kaput")
+            return {"query": query, "results": [{"text": "d", "score": 0.5, "is_ground_truth": False, "rank": 1}]}
+
+    client = TestClient(make_app(FakeIndex()))
+    r = client.post("/search", json={"query": "what is a gene"})
+    assert r.status_code == 200
+    assert r.json() == {"query": "what is a gene",
+                        "results": [{"text": "d", "score": 0.5, "is_ground_truth": False, "rank": 1}]}
+    r = client.post("/search", json={"query": "boom"})
+    assert r.status_code == 500 and r.json()["detail"] == "kaput"
+    assert client.post("/search", json={}).status_code == 422

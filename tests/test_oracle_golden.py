@@ -126,3 +126,32 @@ def test_dropout_mask_statistics_and_determinism():
     frac = float((m1 == 0).mean())
     assert 0.09 < frac < 0.11
     assert set(np.unique(m1)) == {0.0, np.float32(1 / 0.9)}
+
+
+def test_margin_model():
+    """oracle.margin_* vs margin_two_tower.TwoTowerModel(16, 8) run by gen_goldens.py."""
+    z = load("margin_tiny")
+    p = {k: v.requires_grad_(True) for k, v in params(z, "w.").items()}
+    assert set(p) == set(cpu_ref.margin_param_shapes(16, 8))
+    q, d = torch.from_numpy(z["q"]), torch.from_numpy(z["d"])
+    with torch.no_grad():
+        close(cpu_ref.margin_forward(q, d, p, training=False), z["sim"])
+        close(cpu_ref.margin_encode(q, p, "query"), z["enc_q"])
+        close(cpu_ref.margin_encode(d, p, "doc"), z["enc_d"])
+    qn, dn = cpu_ref.margin_forward(q, d, p, training=True)
+    loss = cpu_ref.infonce(qn, dn, temperature=0.1)
+    loss.backward()
+    close(qn.detach(), z["qn"])
+    close(dn.detach(), z["dn"])
+    close(float(loss), z["loss"])
+    for k, t in p.items():
+        close(t.grad, z[f"g.{k}"], rtol=1e-4, atol=1e-6)
+
+
+def test_margin_featurize():
+    z = load("margin_featurize")
+    vocab = {str(w): i for i, w in enumerate(z["words"])}
+    T = int(z["max_length"])
+    for text, emb in zip(z["texts"], z["emb"]):
+        ids = cpu_ref.margin_text_to_ids(str(text), vocab, T)
+        np.testing.assert_array_equal(cpu_ref.ids_to_embedding(ids, z["vecs"]), emb)

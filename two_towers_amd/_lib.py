@@ -68,6 +68,21 @@ class HeadBwdIO(ctypes.Structure):
     ]
 
 
+class Head1FwdIO(ctypes.Structure):
+    _fields_ = [
+        ("x", c_void_p), ("w1", c_void_p), ("b1", c_void_p), ("ln_g", c_void_p), ("ln_b", c_void_p),
+        ("p1", c_void_p), ("mean", c_void_p), ("rstd", c_void_p), ("out", c_void_p),
+    ]
+
+
+class Head1BwdIO(ctypes.Structure):
+    _fields_ = [
+        ("x", c_void_p), ("w1", c_void_p), ("ln_g", c_void_p), ("ln_b", c_void_p), ("p1", c_void_p),
+        ("mean", c_void_p), ("rstd", c_void_p), ("dout", c_void_p), ("dx", c_void_p), ("dw1", c_void_p),
+        ("db1", c_void_p), ("dg", c_void_p), ("dbeta", c_void_p), ("ws", c_void_p),
+    ]
+
+
 # name -> (restype, argtypes). Kept in the order of include/tt_hip.h.
 _SIGS = {
     "tt_version": (ctypes.c_char_p, []),
@@ -90,6 +105,10 @@ _SIGS = {
     "tt_proj_head_fwd": (c_int, [c_int, POINTER(HeadFwdIO), c_int, c_int, c_int, c_float, c_void_p]),
     "tt_proj_head_bwd": (c_int, [c_int, POINTER(HeadBwdIO), c_int, c_int, c_int, c_float, c_void_p]),
     "tt_proj_head_bwd_ws_size": (c_long, [c_int, c_int, c_int]),
+    "tt_proj_head1_fwd": (c_int, [c_int, POINTER(Head1FwdIO), c_long, c_int, c_float, c_float, c_uint32,
+                                  c_void_p]),
+    "tt_proj_head1_bwd": (c_int, [c_int, POINTER(Head1BwdIO), c_long, c_int, c_float, c_uint32, c_void_p]),
+    "tt_proj_head1_bwd_ws_size": (c_long, [c_int, c_long, c_int]),
     "tt_l2norm_fwd": (c_int, [c_int, c_void_p, c_long, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
     "tt_l2norm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_int, c_float, c_void_p, c_int, c_void_p]),
     "tt_infonce_fwd": (c_int, [c_int, c_void_p, c_long, c_void_p, c_long, c_int, c_float, c_float, c_long,

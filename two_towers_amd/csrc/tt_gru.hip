@@ -349,7 +349,7 @@ __global__ __launch_bounds__(512) void gru_bwd_big(BwdArgs a) {
   const int tp = R.dir ? t + 1 : t - 1;
   const bool last = (s == T_ - 1);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, tid = threadIdx.x;
-  const int wm = (wave >> 2) * 128, wn = (wave & 3) * 64;
+  const int wn = (wave & 3) * 64;
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -762,7 +762,8 @@ extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B
   TT_CHECK_ARG(nrec >= 1 && nrec <= 4, "tt_gru_fwd: nrec %d", nrec);
   TT_CHECK_ARG(B > 0 && T > 0 && H > 0, "tt_gru_fwd: bad shape");
   const int esz = dtype == TT_DT_BF16 ? 2 : 4;
-  TT_CHECK_ARG(H % (16 / esz) == 0 && (ldy * esz) % 16 == 0, "tt_gru_fwd: H=%d/ldy=%ld misaligned", H, ldy);
+  // epilogues update 8 consecutive hidden units per thread
+  TT_CHECK_ARG(H % 8 == 0 && (ldy * esz) % 16 == 0, "tt_gru_fwd: H=%d (multiple of 8)/ldy=%ld misaligned", H, ldy);
   TT_CHECK_ARG(drop_p >= 0.f && drop_p < 1.f, "tt_gru_fwd: drop_p");
   TT_CHECK_ARG(tt_ceil_div(B, 128) <= 65535, "tt_gru_fwd: B too large");
   TT_CHECK_ARG(128L * T * std::max(4L * H, ldy) * esz < (1L << 31), "tt_gru_fwd: tile byte offsets exceed 2 GiB");
@@ -803,7 +804,7 @@ extern "C" int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B
   TT_CHECK_ARG(nrec >= 1 && nrec <= 4, "tt_gru_bwd: nrec %d", nrec);
   TT_CHECK_ARG(B > 0 && T > 0 && H > 0, "tt_gru_bwd: bad shape");
   const int esz = dtype == TT_DT_BF16 ? 2 : 4;
-  TT_CHECK_ARG(H % (16 / esz) == 0 && (ldd * esz) % 16 == 0, "tt_gru_bwd: H=%d/ldd=%ld misaligned", H, ldd);
+  TT_CHECK_ARG(H % 8 == 0 && (ldd * esz) % 16 == 0, "tt_gru_bwd: H=%d (multiple of 8)/ldd=%ld misaligned", H, ldd);
   TT_CHECK_ARG(128L * T * ldd * esz < (1L << 31), "tt_gru_bwd: tile byte offsets exceed 2 GiB");
   hipStream_t st = (hipStream_t)stream;
   BwdArgs a{};

@@ -1,6 +1,9 @@
-// Projection head Linear(4h->2h) -> LayerNorm(2h) -> ReLU -> Linear(2h->h):
-// LayerNorm+ReLU kernels and the composite forward/backward built on tt_gemm.
+// Projection heads built on tt_gemm plus fused LayerNorm+ReLU(+Dropout) kernels:
+//   enhanced: Linear(4h->2h) -> LayerNorm(2h) -> ReLU -> Linear(2h->h)
+//   margin:   Linear(2H->H) -> LayerNorm(H) -> ReLU -> Dropout(p), one set of weights
+//             shared by both towers (query and doc rows stacked into one batch).
 #include <algorithm>
+#include <climits>
 
 #include "tt_api.h"
 #include "tt_common.h"
@@ -10,12 +13,15 @@ namespace {
 constexpr int LN_MAXC = 16;  // columns per lane -> up to 1024 columns (h <= 512)
 
 // One wave per row. u = relu((x - mean) * rstd * g + b)
-template <typename T>
+// With drop_thresh != 0 the ReLU output is multiplied by the counter-based dropout
+// mask keep(seed, row, col) / (1 - p) (tt_dropout_scale, recomputed by the backward).
+template <typename T, typename TO>
 __global__ __launch_bounds__(256) void ln_relu_fwd_kernel(const T* __restrict__ x, long rows, int C,
                                                           const float* __restrict__ gam,
                                                           const float* __restrict__ bet, float eps,
-                                                          T* __restrict__ u, float* __restrict__ mean,
-                                                          float* __restrict__ rstd) {
+                                                          TO* __restrict__ u, float* __restrict__ mean,
+                                                          float* __restrict__ rstd, uint32_t drop_seed,
+                                                          uint32_t drop_thresh, float inv_keep) {
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -40,7 +46,11 @@ __global__ __launch_bounds__(256) void ln_relu_fwd_kernel(const T* __restrict__ 
 #pragma unroll
   for (int q = 0; q < LN_MAXC; ++q) {
     const int c = lane + 64 * q;
-    if (c < C) Elt<T>::st(u + row * C + c, fmaxf((v[q] - mu) * rs * gam[c] + bet[c], 0.f));
+    if (c < C) {
+      float o = fmaxf((v[q] - mu) * rs * gam[c] + bet[c], 0.f);
+      if (drop_thresh) o *= tt_dropout_scale(drop_seed, (uint32_t)row, (uint32_t)c, drop_thresh, inv_keep);
+      Elt<TO>::st(u + row * C + c, o);
+    }
   }
   if (lane == 0) {
     mean[row] = mu;
@@ -57,7 +67,8 @@ __global__ __launch_bounds__(256) void ln_relu_bwd_kernel(const float* __restric
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ rstd, long rows, int C,
                                                           int rows_per_block, T* __restrict__ dx,
-                                                          float* __restrict__ part) {
+                                                          float* __restrict__ part, uint32_t drop_seed,
+                                                          uint32_t drop_thresh, float inv_keep) {
   __shared__ float red[4][3][LN_MAXC * 64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float pg[LN_MAXC], pb[LN_MAXC], pd[LN_MAXC];
@@ -77,6 +88,7 @@ __global__ __launch_bounds__(256) void ln_relu_bwd_kernel(const float* __restric
         xh[q] = (Elt<T>::ld(x + row * C + c) - mu) * rs;
         const float a = xh[q] * gam[c] + bet[c];
         da[q] = a > 0.f ? du[row * C + c] : 0.f;
+        if (drop_thresh) da[q] *= tt_dropout_scale(drop_seed, (uint32_t)row, (uint32_t)c, drop_thresh, inv_keep);
         const float dxh = da[q] * gam[c];
         s1 += dxh;
         s2 += dxh * xh[q];
@@ -151,11 +163,13 @@ extern "C" int tt_proj_head_fwd(int dtype, const tt_head_fwd_io* io, int ntower,
   for (int i = 0; i < ntower; ++i) {
     dim3 grid(tt_ceil_div(B, 4));
     if (dtype == TT_DT_BF16)
-      hipLaunchKernelGGL(ln_relu_fwd_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)io[i].p1, (long)B,
-                         2 * h, io[i].ln_g, io[i].ln_b, ln_eps, (bf16_t*)io[i].u, io[i].mean, io[i].rstd);
+      hipLaunchKernelGGL((ln_relu_fwd_kernel<bf16_t, bf16_t>), grid, dim3(256), 0, st, (const bf16_t*)io[i].p1,
+                         (long)B, 2 * h, io[i].ln_g, io[i].ln_b, ln_eps, (bf16_t*)io[i].u, io[i].mean, io[i].rstd,
+                         0u, 0u, 1.f);
     else
-      hipLaunchKernelGGL(ln_relu_fwd_kernel<float>, grid, dim3(256), 0, st, (const float*)io[i].p1, (long)B, 2 * h,
-                         io[i].ln_g, io[i].ln_b, ln_eps, (float*)io[i].u, io[i].mean, io[i].rstd);
+      hipLaunchKernelGGL((ln_relu_fwd_kernel<float, float>), grid, dim3(256), 0, st, (const float*)io[i].p1,
+                         (long)B, 2 * h, io[i].ln_g, io[i].ln_b, ln_eps, (float*)io[i].u, io[i].mean, io[i].rstd,
+                         0u, 0u, 1.f);
     TT_CHECK_LAUNCH("ln_relu_fwd_kernel");
   }
   // out = u w2^T + b2  [B, h] fp32
@@ -200,10 +214,10 @@ extern "C" int tt_proj_head_bwd(int dtype, const tt_head_bwd_io* io, int ntower,
     // LayerNorm + ReLU backward -> dp1, partial (dgamma, dbeta, db1)
     if (dtype == TT_DT_BF16)
       hipLaunchKernelGGL(ln_relu_bwd_kernel<bf16_t>, dim3(nblk), dim3(256), 0, st, du, (const bf16_t*)q.p1, q.ln_g,
-                         q.ln_b, q.mean, q.rstd, (long)B, C, LN_ROWS_PER_BLOCK, (bf16_t*)dp1, part);
+                         q.ln_b, q.mean, q.rstd, (long)B, C, LN_ROWS_PER_BLOCK, (bf16_t*)dp1, part, 0u, 0u, 1.f);
     else
       hipLaunchKernelGGL(ln_relu_bwd_kernel<float>, dim3(nblk), dim3(256), 0, st, du, (const float*)q.p1, q.ln_g,
-                         q.ln_b, q.mean, q.rstd, (long)B, C, LN_ROWS_PER_BLOCK, (float*)dp1, part);
+                         q.ln_b, q.mean, q.rstd, (long)B, C, LN_ROWS_PER_BLOCK, (float*)dp1, part, 0u, 0u, 1.f);
     TT_CHECK_LAUNCH("ln_relu_bwd_kernel");
     TT_PROPAGATE(tt_colsum(part, nblk, C, 3L * C, q.dg, 0, stream));
     TT_PROPAGATE(tt_colsum(part + C, nblk, C, 3L * C, q.dbeta, 0, stream));
@@ -223,6 +237,106 @@ extern "C" int tt_proj_head_bwd(int dtype, const tt_head_bwd_io* io, int ntower,
       TT_PROPAGATE(tt_gemm(dtype, TT_DT_F32, 0, 1, B, 2 * C, C, &g, 1, C, 2 * C, 2 * C, 1.f, 0, 0, 0, 0, 0.f, 1,
                            nullptr, stream));
     }
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------ margin head
+namespace {
+
+inline long head1_ws_layout(int dtype, long rows, int C, long* o_dp1, long* o_part, long* o_sk) {
+  const int esz = dtype == TT_DT_BF16 ? 2 : 4;
+  auto al = [](long x) { return (x + 255) & ~255L; };
+  long off = 0;
+  *o_dp1 = off;  off = al(off + rows * C * esz);
+  const long nblk = tt_ceil_div(rows, LN_ROWS_PER_BLOCK);
+  *o_part = off; off = al(off + nblk * 3L * C * 4);
+  const int sp = tt_gemm_pick_splits(C, 2 * C, (int)rows, 1);
+  *o_sk = off;   off = al(off + tt_gemm_ws_size(C, 2 * C, 1, sp) * 4);
+  return off;
+}
+
+inline void drop_params(float p, uint32_t* thresh, float* inv_keep) {
+  // keep iff (hash >> 8) >= thresh, i.e. P(drop) = thresh / 2^24 (tt_dropout_scale)
+  *thresh = p > 0.f ? (uint32_t)(p * 16777216.0f + 0.5f) : 0u;
+  *inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
+}
+
+}  // namespace
+
+extern "C" long tt_proj_head1_bwd_ws_size(int dtype, long rows, int C) {
+  long a, b, c;
+  return head1_ws_layout(dtype, rows, C, &a, &b, &c);
+}
+
+extern "C" int tt_proj_head1_fwd(int dtype, const tt_head1_fwd_io* io, long rows, int C, float ln_eps,
+                                 float drop_p, uint32_t drop_seed, void* stream) {
+  TT_CHECK_ARG(C >= 1 && C <= 64 * LN_MAXC, "tt_proj_head1_fwd: C=%d out of range", C);
+  TT_CHECK_ARG(rows >= 1 && rows <= INT_MAX, "tt_proj_head1_fwd: rows");
+  TT_CHECK_ARG(drop_p >= 0.f && drop_p < 1.f, "tt_proj_head1_fwd: drop_p");
+  hipStream_t st = (hipStream_t)stream;
+  // p1 = x w1^T + b1   [rows, C]
+  tt_gemm_batch g{};
+  g.a[0] = io->x; g.b[0] = io->w1; g.c[0] = io->p1; g.bias[0] = io->b1;
+  TT_PROPAGATE(tt_gemm(dtype, dtype, 0, 0, (int)rows, C, 2 * C, &g, 1, 2 * C, 2 * C, C, 1.f, 0, 0, 0, 0, 0.f, 1,
+                       nullptr, stream));
+  uint32_t thresh;
+  float inv_keep;
+  drop_params(drop_p, &thresh, &inv_keep);
+  dim3 grid(tt_ceil_div(rows, 4));
+  if (dtype == TT_DT_BF16)
+    hipLaunchKernelGGL((ln_relu_fwd_kernel<bf16_t, float>), grid, dim3(256), 0, st, (const bf16_t*)io->p1, rows, C,
+                       io->ln_g, io->ln_b, ln_eps, io->out, io->mean, io->rstd, drop_seed, thresh, inv_keep);
+  else
+    hipLaunchKernelGGL((ln_relu_fwd_kernel<float, float>), grid, dim3(256), 0, st, (const float*)io->p1, rows, C,
+                       io->ln_g, io->ln_b, ln_eps, io->out, io->mean, io->rstd, drop_seed, thresh, inv_keep);
+  TT_CHECK_LAUNCH("ln_relu_fwd_kernel");
+  return 0;
+}
+
+extern "C" int tt_proj_head1_bwd(int dtype, const tt_head1_bwd_io* io, long rows, int C, float drop_p,
+                                 uint32_t drop_seed, void* stream) {
+  TT_CHECK_ARG(C >= 1 && C <= 64 * LN_MAXC, "tt_proj_head1_bwd: C=%d out of range", C);
+  TT_CHECK_ARG(rows >= 1 && rows <= INT_MAX, "tt_proj_head1_bwd: rows");
+  TT_CHECK_ARG(drop_p >= 0.f && drop_p < 1.f, "tt_proj_head1_bwd: drop_p");
+  hipStream_t st = (hipStream_t)stream;
+  long o_dp1, o_part, o_sk;
+  head1_ws_layout(dtype, rows, C, &o_dp1, &o_part, &o_sk);
+  char* ws = static_cast<char*>(io->ws);
+  void* dp1 = ws + o_dp1;
+  float* part = reinterpret_cast<float*>(ws + o_part);
+  float* sk = reinterpret_cast<float*>(ws + o_sk);
+  uint32_t thresh;
+  float inv_keep;
+  drop_params(drop_p, &thresh, &inv_keep);
+  const long nblk = tt_ceil_div(rows, LN_ROWS_PER_BLOCK);
+  // Dropout + ReLU + LayerNorm backward -> dp1, partial (dgamma, dbeta, db1)
+  if (dtype == TT_DT_BF16)
+    hipLaunchKernelGGL(ln_relu_bwd_kernel<bf16_t>, dim3(nblk), dim3(256), 0, st, io->dout, (const bf16_t*)io->p1,
+                       io->ln_g, io->ln_b, io->mean, io->rstd, rows, C, LN_ROWS_PER_BLOCK, (bf16_t*)dp1, part,
+                       drop_seed, thresh, inv_keep);
+  else
+    hipLaunchKernelGGL(ln_relu_bwd_kernel<float>, dim3(nblk), dim3(256), 0, st, io->dout, (const float*)io->p1,
+                       io->ln_g, io->ln_b, io->mean, io->rstd, rows, C, LN_ROWS_PER_BLOCK, (float*)dp1, part,
+                       drop_seed, thresh, inv_keep);
+  TT_CHECK_LAUNCH("ln_relu_bwd_kernel");
+  TT_PROPAGATE(tt_colsum(part, nblk, C, 3L * C, io->dg, 0, stream));
+  TT_PROPAGATE(tt_colsum(part + C, nblk, C, 3L * C, io->dbeta, 0, stream));
+  TT_PROPAGATE(tt_colsum(part + 2 * C, nblk, C, 3L * C, io->db1, 0, stream));
+  // dW1 = dp1^T x   [C, 2C]: the sum over all rows is the sum over both towers
+  {
+    tt_gemm_batch g{};
+    g.a[0] = dp1; g.b[0] = io->x; g.c[0] = io->dw1;
+    const int sp = tt_gemm_pick_splits(C, 2 * C, (int)rows, 1);
+    TT_PROPAGATE(tt_gemm(dtype, TT_DT_F32, 1, 1, C, 2 * C, (int)rows, &g, 1, C, 2 * C, 2 * C, 1.f, 0, 0, 0, 0, 0.f,
+                         sp, sk, stream));
+  }
+  // dx = dp1 w1   [rows, 2C]
+  {
+    tt_gemm_batch g{};
+    g.a[0] = dp1; g.b[0] = io->w1; g.c[0] = io->dx;
+    TT_PROPAGATE(tt_gemm(dtype, TT_DT_F32, 0, 1, (int)rows, 2 * C, C, &g, 1, C, 2 * C, 2 * C, 1.f, 0, 0, 0, 0, 0.f, 1,
+                         nullptr, stream));
   }
   return 0;
 }

@@ -449,7 +449,7 @@ extern "C" long tt_hardneg_ws_size(int dtype, long bq, long nd) {
 
 extern "C" int tt_hardneg_topk(int dtype, const void* qn, long bq, const void* dn, long nd, int h, long label_offset,
                                int k, int32_t* idx, float* val, void* ws, void* stream) {
-  TT_CHECK_ARG(k >= 1 && k <= TOPK_MAX && k < nd, "tt_hardneg_topk: k=%d", k);
+  TT_CHECK_ARG(k >= 1 && k <= TOPK_MAX && k <= nd, "tt_hardneg_topk: k=%d (nd=%ld)", k, nd);
   TT_CHECK_ARG(label_offset < 0 || label_offset + bq <= nd, "tt_hardneg_topk: labels outside [0, nd)");
   if (bq == 0) return 0;
   float* S = static_cast<float*>(ws);

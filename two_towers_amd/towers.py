@@ -52,6 +52,11 @@ class TowerCfg:
     h: int  # output dim (= hidden_dim)
     dtype: torch.dtype
     drop_p: float  # dropout between GRU layers (0 in eval)
+    head: str = "proj2"  # "proj2": per-tower enhanced head; "none": return cat(h_fwd, h_rev) [B, 2H]
+
+    @property
+    def nparams(self) -> int:
+        return PARAMS_PER_TOWER if self.head == "proj2" else len(GRU_NAMES)
 
 
 class _Packed:
@@ -78,6 +83,8 @@ class _Packed:
             self.bias.append(torch.cat(bs).float().contiguous())
             self.whh.append([g[f"weight_hh_l{layer}{s}"].to(dt).contiguous() for s in ("", "_reverse")])
             self.bhn.append([g[f"bias_hh_l{layer}{s}"][2 * H:].float().contiguous() for s in ("", "_reverse")])
+        if cfg.head == "none":
+            return
         # The projection head always runs in fp32 (HEAD_DT): it is <1% of the FLOPs, and its
         # backward is where the batch-wide cancellation of the contrastive-loss gradient
         # would otherwise lose most of its precision to a bf16 cast.
@@ -230,7 +237,9 @@ def _weight_grads(cfg, B, T, dG, Xin, K, ldx, Y):
 
 
 class TowersFn(torch.autograd.Function):
-    """(x_0..x_{n-1}, params...) -> (vec_0..vec_{n-1}), vec_i = tower_i(x_i) as [B, h] fp32."""
+    """(x_0..x_{n-1}, params...) -> (vec_0..vec_{n-1}), vec_i = tower_i(x_i) as [B, h] fp32
+    (cfg.head "proj2"), or the final bidirectional state cat(h_fwd, h_rev) as [B, 2H] fp32
+    (cfg.head "none": margin_two_tower.py:59-61, the head runs outside)."""
 
     @staticmethod
     def forward(ctx, cfg: TowerCfg, table, *args):
@@ -244,7 +253,8 @@ class TowersFn(torch.autograd.Function):
             if x.shape[0] != B or x.shape[1] != T:
                 raise ValueError("query and doc inputs must share [B, T] in one fused call")
         Ep = ops.pad_cols(E, dt)
-        packs = [_Packed(params[i * PARAMS_PER_TOWER:(i + 1) * PARAMS_PER_TOWER], cfg, Ep) for i in range(n)]
+        npt = cfg.nparams
+        packs = [_Packed(params[i * npt:(i + 1) * npt], cfg, Ep) for i in range(n)]
         X0 = [featurize(x, table, Ep, dt) for x in xs]
         train_drop = cfg.drop_p > 0.0
         seeds = [int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) for _ in range(n)] if train_drop else [0] * n
@@ -256,6 +266,13 @@ class TowersFn(torch.autograd.Function):
         for ti in range(n):
             y = Y1[ti].view(B, T, 2 * H)
             hcat.append(torch.cat([y[:, T - 1, :H], y[:, 0, H:]], 1).to(HEAD_DT).contiguous())
+        ctx.cfg = cfg
+        ctx.dims = (B, T, Ep)
+        ctx.seeds = seeds
+        ctx.packs = packs
+        if cfg.head == "none":
+            ctx.acts = (X0, Y0, X1, S0, Y1, S1, None, None, None, None, None)
+            return tuple(hcat)
         outs, p1s, means, rstds, us = [], [], [], [], []
         io = (HeadFwdIO * n)()
         for ti in range(n):
@@ -272,10 +289,6 @@ class TowersFn(torch.autograd.Function):
                                                      rstd.data_ptr(), u.data_ptr(), out.data_ptr())
             outs.append(out); p1s.append(p1); means.append(mean); rstds.append(rstd); us.append(u)
         call("tt_proj_head_fwd", dtype_code(HEAD_DT), io, n, B, h, LN_EPS, stream_ptr(dev))
-        ctx.cfg = cfg
-        ctx.dims = (B, T, Ep)
-        ctx.seeds = seeds
-        ctx.packs = packs
         ctx.acts = (X0, Y0, X1, S0, Y1, S1, hcat, p1s, means, rstds, us)
         return tuple(outs)
 
@@ -290,10 +303,17 @@ class TowersFn(torch.autograd.Function):
         lib = _lib.load()
         st = stream_ptr(dev)
         # ---- projection head
-        head_grads = []
+        head_grads = [[] for _ in range(n)]
         dhcat = []
-        ws = _alloc((lib.tt_proj_head_bwd_ws_size(dtype_code(HEAD_DT), B, h),), torch.uint8, dev)
-        for ti in range(n):
+        if cfg.head == "none":
+            for ti in range(n):
+                g = gouts[ti]
+                dhcat.append(torch.zeros(B, 2 * H, dtype=torch.float32, device=dev) if g is None
+                             else g.float().contiguous())
+        ws = None
+        if cfg.head == "proj2":
+            ws = _alloc((lib.tt_proj_head_bwd_ws_size(dtype_code(HEAD_DT), B, h),), torch.uint8, dev)
+        for ti in range(n if cfg.head == "proj2" else 0):
             g = gouts[ti]
             g = torch.zeros(B, h, dtype=torch.float32, device=dev) if g is None else g.float().contiguous()
             pk = packs[ti]
@@ -313,7 +333,7 @@ class TowersFn(torch.autograd.Function):
                                                                dbeta.data_ptr(), dw2.data_ptr(), db2.data_ptr())
             io.ws = ws.data_ptr()
             call("tt_proj_head_bwd", dtype_code(HEAD_DT), ctypes.byref(io), 1, B, h, LN_EPS, st)
-            head_grads.append([dw1, db1, dg, dbeta, dw2, db2])
+            head_grads[ti] = [dw1, db1, dg, dbeta, dw2, db2]
             dhcat.append(dx)
         # ---- GRU layer 1: dfinal enters at the last processed step of each direction
         dG1, dbih1, dbhh1 = _gru_layer_bwd(cfg, 1, B, T, S1, Y1, None, dhcat, packs)
@@ -358,4 +378,7 @@ class TowersFn(torch.autograd.Function):
 
 
 def run_towers(cfg: TowerCfg, table, xs, params):
+    if cfg.H % 8:
+        raise ValueError(f"GRU hidden size {cfg.H} must be a multiple of 8 on the HIP path "
+                         "(the step epilogues update 8 consecutive units per thread)")
     return TowersFn.apply(cfg, table, *xs, *params)

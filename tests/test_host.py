@@ -211,3 +211,105 @@ def test_search_http_contract():
     r = client.post("/search", json={"query": "boom"})
     assert r.status_code == 500 and r.json()["detail"] == "kaput"
     assert client.post("/search", json={}).status_code == 422
+
+
+def test_word2vec_binary_and_text_formats(tmp_path):
+    """w2v.read_word2vec_format on hand-built word2vec.c layouts (header 'V E', then
+    'word ' + E little-endian float32 [+ '\\n'] or 'word v1 .. vE\\n')."""
+    import struct
+
+    from two_towers_amd import w2v
+    raw = (b"4 2\n" + b"hello " + struct.pack("<2f", 1.0, -2.5) + b"\n" + b"World " + struct.pack("<2f", 0.5, 3.0)
+           + b"caf\xc3\xa9 " + struct.pack("<2f", 7.0, 8.0) + b"\n" + b"hello " + struct.pack("<2f", 9.0, 9.0) + b"\n")
+    p = tmp_path / "v.bin"
+    p.write_bytes(raw)
+    v = w2v.read_word2vec_format(str(p))
+    assert list(v.index) == ["hello", "World", "café"]  # duplicate: first occurrence wins
+    np.testing.assert_array_equal(v.vectors, np.array([[1, -2.5], [0.5, 3], [7, 8]], np.float32))
+    assert len(w2v.read_word2vec_format(str(p), limit=2)) == 2
+    t = tmp_path / "v.txt"
+    t.write_text("2 3\nfoo 1 2 3\nbar -1.5 0 1e-3\n", encoding="utf-8")
+    vt = w2v.read_word2vec_format(str(t))
+    assert list(vt.index) == ["foo", "bar"]
+    np.testing.assert_array_equal(vt.vectors, np.array([[1, 2, 3], [-1.5, 0, 1e-3]], np.float32))
+    for binary in (True, False):
+        out = tmp_path / f"rt{int(binary)}"
+        w2v.write_word2vec_format(v, str(out), binary=binary)
+        back = w2v.read_word2vec_format(str(out))
+        assert list(back.index) == list(v.index)
+        np.testing.assert_array_equal(back.vectors, v.vectors)
+    (tmp_path / "bad.bin").write_bytes(b"2 4\nx " + struct.pack("<2f", 1, 2))
+    with pytest.raises(ValueError, match="truncated"):
+        w2v.read_word2vec_format(str(tmp_path / "bad.bin"), binary=True)
+
+
+def test_word2vec_store_roundtrip(tmp_path):
+    from two_towers_amd import w2v
+    rng = np.random.default_rng(0)
+    words = [f"w{i}" for i in range(1000)] + ["naïve", "日本"]
+    v = tta.Vocab(words, rng.standard_normal((len(words), 12)).astype(np.float32))
+    w2v.save_store(v, str(tmp_path / "store"))
+    back = w2v.load_store(str(tmp_path / "store"))
+    assert back.index == v.index and isinstance(back.vectors, np.memmap)
+    np.testing.assert_array_equal(np.asarray(back.vectors), v.vectors)
+    tab = back.device_table("cpu")
+    assert torch.equal(tab, torch.from_numpy(v.vectors))
+    assert "日本" in back and np.array_equal(back["naïve"], v.vectors[1000])
+
+
+def test_pretokenize_matches_reference_featurization(tmp_path):
+    """Offline id files reproduce EnhancedDataset / SimpleDataset rows of the reference
+    (the featurize / margin_featurize fixtures), through a fork pool and the id store."""
+    import json
+
+    from two_towers_amd import pretok
+    for fixture, tok in (("featurize", "enhanced"), ("margin_featurize", "margin")):
+        z = np.load(os.path.join(GOLD, fixture + ".npz"), allow_pickle=False)
+        vocab = tta.Vocab([str(w) for w in z["words"]], z["vecs"])
+        texts = [str(t) for t in z["texts"]] * 3
+        T = int(z["max_length"])
+        out = tmp_path / tok
+        meta = pretok.pretokenize(texts, texts[::-1], vocab, str(out), T, tok, workers=2)
+        assert meta["n"] == len(texts) and meta["tokenizer"] == tok
+        ds = pretok.PairIds(str(out), vocab)
+        emb = np.concatenate([z["emb"]] * 3)
+        zero = np.zeros((1, vocab.vector_size), np.float32)
+        table = np.concatenate([vocab.vectors, zero])  # row -1 -> zero row
+        for i in range(len(ds)):
+            q, d = ds[i]
+            np.testing.assert_array_equal(table[q.numpy()], emb[i])
+            np.testing.assert_array_equal(table[d.numpy()], emb[len(texts) - 1 - i])
+        with open(out / "meta.json") as f:
+            assert json.load(f)["vocab_sha1"] == pretok.vocab_sha1(vocab)
+    other = tta.Vocab(["x"], np.zeros((1, 8), np.float32))
+    with pytest.raises(ValueError, match="different vocabulary"):
+        pretok.PairIds(str(tmp_path / "enhanced"), other)
+
+
+def test_pair_id_batches_shard_global_batches(tmp_path):
+    from two_towers_amd import pretok
+    vocab = tta.Vocab([f"t{i}" for i in range(50)], np.ones((50, 4), np.float32))
+    texts = [f"t{i % 50} t{(i * 7) % 50}" for i in range(103)]
+    pretok.pretokenize(texts, texts, vocab, str(tmp_path), 4, "enhanced", workers=1)
+    ds = pretok.PairIds(str(tmp_path))
+    full = [q for q, _ in ds.batches(8, device="cpu", seed=3, world=1)]
+    assert len(full) == 103 // 8
+    r0 = [q for q, _ in ds.batches(4, device="cpu", seed=3, rank=0, world=2)]
+    r1 = [q for q, _ in ds.batches(4, device="cpu", seed=3, rank=1, world=2)]
+    assert len(r0) == len(r1) == 103 // 8
+    for a, b, g in zip(r0, r1, full):  # the two ranks' rows are exactly the global batch
+        assert sorted(map(tuple, torch.cat([a, b]).tolist())) == sorted(map(tuple, g.tolist()))
+
+
+def test_read_pairs_formats(tmp_path):
+    import json
+
+    from two_towers_amd import pretok
+    rows = [{"query": "q1", "passages": {"passage_text": ["a", "b", "c"], "is_selected": [0, 1, 1]}},
+            {"query": "", "passages": {"passage_text": ["x"], "is_selected": [1]}},
+            {"query": "q3"},
+            {"query": "q4", "passages": {"passage_text": ["d"], "is_selected": [1]}}]
+    (tmp_path / "p.jsonl").write_text("\n".join(json.dumps(r) for r in rows) + "\n")
+    assert pretok.read_pairs(str(tmp_path / "p.jsonl")) == (["q1", "q1", "q4"], ["b", "c", "d"])
+    (tmp_path / "p.tsv").write_text("q1\tdoc one\nq2\tdoc\ttwo\n\n")
+    assert pretok.read_pairs(str(tmp_path / "p.tsv")) == (["q1", "q2"], ["doc one", "doc\ttwo"])

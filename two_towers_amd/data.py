@@ -88,8 +88,15 @@ class Vocab:
         z = np.load(path, allow_pickle=False)
         return cls([str(w) for w in z["words"]], z["vectors"])
 
-    def device_table(self, device="cuda") -> torch.Tensor:
-        return torch.from_numpy(self.vectors).to(device)
+    def device_table(self, device="cuda", dtype=torch.float32) -> torch.Tensor:
+        """[V, E] table on the device, uploaded in 64 MiB slices (the host array may be a
+        read-only memory map of a multi-GB store: w2v.load_store)."""
+        V, E = self.vectors.shape
+        out = torch.empty(V, E, dtype=dtype, device=device)
+        step = max(1, (64 << 20) // max(4 * E, 1))
+        for i in range(0, V, step):
+            out[i:i + step] = torch.from_numpy(np.array(self.vectors[i:i + step], dtype=np.float32)).to(device, dtype)
+        return out
 
 
 def encode_ids(text: str, vocab, max_length: int = 30) -> List[int]:

@@ -243,6 +243,16 @@ int tt_hardneg_topk(int dtype, const void* qn, long bq, const void* dn, long nd,
                     long label_offset, int k, int32_t* idx, float* val, void* ws, void* stream);
 long tt_hardneg_ws_size(int dtype, long bq, long nd);
 
+/* Serving search (server/python-api/app.py:94-101: F.cosine_similarity of one encoded
+ * query against every cached document row, then torch.topk): qn [Q, h] fp32 normalised
+ * queries, dn [N, h] dtype normalised documents (resident), top-k (1 <= k <= min(16, N))
+ * indices/scores per query, value descending, ties towards the lower document index.
+ * Q <= 64: one fused pass over dn per 8 queries (per-lane top-k, no score matrix);
+ * larger Q: cosine GEMM + column-split top-k. h % 8 == 0. ws: tt_search_ws_size bytes. */
+int tt_search_topk(int dtype, const float* qn, long Q, const void* dn, long N, int h, int k,
+                   int32_t* idx, float* val, void* ws, void* stream);
+long tt_search_ws_size(int dtype, long Q, long N, int h, int k);
+
 /* MarginRankingLoss with explicit negatives (enhanced_two_tower.py:102-121) on
  * normalised vectors: pos_i = qn_i.dn_{label_offset+i}, negm_i = mean_j qn_i.dn_{idx[i,j]},
  * row_loss_i = max(margin - pos_i + negm_i, 0). Negatives are rows of dn. */

@@ -120,6 +120,9 @@ _SIGS = {
     "tt_hardneg_topk": (c_int, [c_int, c_void_p, c_long, c_void_p, c_long, c_int, c_long, c_int, c_void_p,
                                 c_void_p, c_void_p, c_void_p]),
     "tt_hardneg_ws_size": (c_long, [c_int, c_long, c_long]),
+    "tt_search_topk": (c_int, [c_int, c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_void_p, c_void_p,
+                               c_void_p, c_void_p]),
+    "tt_search_ws_size": (c_long, [c_int, c_long, c_long, c_int, c_int]),
     "tt_margin_fwd": (c_int, [c_void_p, c_long, c_void_p, c_long, c_int, c_long, c_void_p, c_int, c_float,
                               c_void_p, c_void_p]),
     "tt_margin_bwd": (c_int, [c_void_p, c_long, c_void_p, c_long, c_int, c_long, c_void_p, c_int, c_float,

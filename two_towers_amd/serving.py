@@ -11,8 +11,8 @@ SearchIndex does the same on the HIP path, laid out for serving:
     margin_ids rows, one launch sequence per batch of up to 4096 documents);
   - the cached matrix is stored already L2-normalised (eps 1e-8, F.cosine_similarity's)
     in the scoring dtype and stays resident in HBM, so a request is one query encode,
-    one GEMV/GEMM against the resident matrix and one top-k kernel (tt_hardneg_topk with
-    no column masked); batches of queries go through the same launches;
+    one fused pass over the resident matrix (tt_search_topk: per-lane scores and top-k,
+    no score matrix, for up to 64 queries at once; a GEMM + column-split top-k beyond);
   - ties rank the lower document index first (torch.topk leaves them unspecified).
 
 make_app(index) builds the FastAPI app with the reference's request/response models
@@ -104,22 +104,22 @@ class SearchIndex:
         nd = self.doc_normed.shape[0]
         if not 1 <= k <= min(16, nd):
             raise ValueError(f"top_k={k} needs 1 <= k <= min(16, {nd})")
-        qn, _, _ = ops.l2norm_fwd(query_vecs.float().contiguous(), COS_EPS, self.score_dtype, want_f32=False)
+        qn, _, _ = ops.l2norm_fwd(query_vecs.float().contiguous(), COS_EPS, torch.float32)
         Q, h = qn.shape
         idx = torch.empty(Q, k, dtype=torch.int32, device=qn.device)
         val = torch.empty(Q, k, dtype=torch.float32, device=qn.device)
         lib = _lib.load()
-        # score matrix chunks of at most 256 MiB
-        step = max(1, min(Q, (64 << 20) // max(nd, 1)))
+        dc = dtype_code(self.score_dtype)
+        # large query batches go through a score block of at most 4 GiB per chunk
+        step = Q if Q <= 64 else max(65, min(Q, (1 << 30) // max(nd, 1)))
         esz = 2 if self.score_dtype == torch.bfloat16 else 4
         for r0 in range(0, Q, step):
             r1 = min(Q, r0 + step)
-            ws = torch.empty(lib.tt_hardneg_ws_size(dtype_code(self.score_dtype), r1 - r0, nd), dtype=torch.uint8,
+            ws = torch.empty(max(lib.tt_search_ws_size(dc, r1 - r0, nd, h, k), 1), dtype=torch.uint8,
                              device=qn.device)
-            with timing.region("search_topk", 1, 2.0 * (r1 - r0) * nd * h, float(esz * ((r1 - r0) + nd) * h)):
-                call("tt_hardneg_topk", dtype_code(self.score_dtype), qn[r0:r1].data_ptr(), r1 - r0,
-                     self.doc_normed.data_ptr(), nd, h, -1, k, idx[r0:r1].data_ptr(), val[r0:r1].data_ptr(),
-                     ws.data_ptr(), stream_ptr(qn.device))
+            with timing.region("search_topk", 1, 2.0 * (r1 - r0) * nd * h, float(esz * nd * h + 4 * (r1 - r0) * h)):
+                call("tt_search_topk", dc, qn[r0:r1].data_ptr(), r1 - r0, self.doc_normed.data_ptr(), nd, h, k,
+                     idx[r0:r1].data_ptr(), val[r0:r1].data_ptr(), ws.data_ptr(), stream_ptr(qn.device))
         return idx.long(), val
 
     def search_batch(self, queries: Sequence[str], top_k: int = TOP_K):

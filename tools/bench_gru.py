@@ -100,6 +100,8 @@ def main():
         print(json.dumps({"bwd_rows": v, "ms": round(ms, 3)}), flush=True)
         del brecs, bkeep
     for v in a.variants.split(","):
+        if not v:
+            continue
         kind, dbg, *depth = v.split(":")
         os.environ["TT_GRU_STEP"] = "1" if kind == "step" else "0"
         os.environ["TT_GRU_DBG"] = dbg

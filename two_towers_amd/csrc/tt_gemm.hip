@@ -43,6 +43,7 @@ struct GemmArgs {
   int force_regstage;
   int bias_vec_ok;  // every bias pointer 16-byte aligned
   int stream_out;   // write-through (sc1) output stores: big outputs
+  int dbg;          // timing diagnostics (env TT_GEMM_DBG): 1 = persistent epilogue issues no stores
 };
 
 constexpr int BM = 128, BN = 128;  // tile of the register-staged / small path
@@ -377,7 +378,8 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
             v[e] = x;
           }
           TO* dst = C + (long)gm * g.ldc + gn;
-          if (gn + 8 <= g.N && g.vec_ok) {
+          if (g.dbg & 1) {
+          } else if (gn + 8 <= g.N && g.vec_ok) {
             if (g.stream_out)
               st8_sc1(crs, (int)(((long)(gm - m0) * g.ldc + (gn - n0)) * (long)sizeof(TO)), v, (TO*)nullptr);
             else
@@ -560,6 +562,8 @@ extern "C" int tt_gemm(int dtype, int out_dtype, int a_kouter, int b_kouter, int
     // outputs far larger than the L2s are streamed past them (sc1); ld*rows must
     // stay addressable by a 32-bit per-tile byte offset
     g.stream_out = ok && (long)m * n * osz >= (64L << 20) && (long)256 * ldc * osz < (1L << 31);
+    if (const char* e = getenv("TT_GEMM_STREAM_OUT")) g.stream_out = g.stream_out && atoi(e) != 0;
+    if (const char* e = getenv("TT_GEMM_DBG")) g.dbg = atoi(e);
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
   TT_CHECK_ARG((long)tt_ceil_div(m, 128) * tt_ceil_div(n, 128) * nbatch * splits < (1L << 31), "tt_gemm: too many tiles");

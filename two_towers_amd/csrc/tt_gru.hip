@@ -28,8 +28,7 @@ struct FwdArgs {
   int s;
   uint32_t drop_thresh;
   float inv_keep;
-  int dbg;  // diagnostics (env TT_GRU_DBG): 1 no stores, 2 no G loads, 4 no MFMA, 8 no Whh stream,
-            // 16 no epilogue (persistent kernel)
+  int dbg;  // diagnostics (env TT_GRU_DBG): 1 no stores, 2 no G loads, 4 no MFMA, 8 no Whh stream
 };
 
 struct BwdRec {
@@ -534,9 +533,9 @@ TT_DEV void fwd_store_b(char* img, const WTile& r) {
 // D-1 tiles ago) into the other stage.
 template <int D>
 TT_DEV void fwd_kstep(const bf16_t* W, int H, int Q, int q, int kt, bool mm, const char* hb, char* bst, int& it,
-                      int wm, int wn, f32x4 (&acc)[2][3], WTile& X, WTile& Y, int dbg) {
-  if (!(dbg & 8)) fwd_load_b(W, H, (q + D) % Q, Y);
-  if (mm && !(dbg & 4)) {  // h_{-1} = 0: the first step has no recurrent term
+                      int wm, int wn, f32x4 (&acc)[2][3], WTile& X, WTile& Y) {
+  fwd_load_b(W, H, (q + D) % Q, Y);
+  if (mm) {  // h_{-1} = 0: the first step has no recurrent term
     const char* ia = hb + kt * (PR * ttg::KTB);
     const char* ib = bst + (it & 1) * P_BST;
 #pragma unroll
@@ -621,7 +620,7 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
 #pragma unroll
           for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         // ring of D register sets: iteration q reads set (q+1)%D, refills set q%D
-#define TT_KS(j, X, Y) fwd_kstep<D>(W, H, Q, blk * nkt + kt + j, kt + j, s > 0, hb, bst, it, wm, wn, acc, X, Y, a.dbg)
+#define TT_KS(j, X, Y) fwd_kstep<D>(W, H, Q, blk * nkt + kt + j, kt + j, s > 0, hb, bst, it, wm, wn, acc, X, Y)
         if constexpr (D == 1) {
           for (int kt = 0; kt < nkt; ++kt) TT_KS(0, r0, r0);
         } else if constexpr (D == 2) {
@@ -630,7 +629,6 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
           for (int kt = 0; kt < nkt; kt += 4) { TT_KS(0, r1, r0); TT_KS(1, r2, r1); TT_KS(2, r3, r2); TT_KS(3, r0, r3); }
         }
 #undef TT_KS
-        if (a.dbg & 16) continue;  // timing only: no epilogue
         // gates -> LDS (fp32), then per-thread rows
 #pragma unroll
         for (int i = 0; i < 2; ++i)

@@ -121,7 +121,7 @@ __global__ __launch_bounds__(256) void ln_relu_bwd_kernel(const float* __restric
   }
 }
 
-constexpr int LN_ROWS_PER_BLOCK = 64;
+constexpr int LN_ROWS_PER_BLOCK = 16;  // 512 blocks at B 8192: fills the chip
 
 inline long head_ws_layout(int dtype, int B, int h, long* o_dout, long* o_du, long* o_dp1, long* o_part,
                            long* o_sk) {

@@ -6,6 +6,7 @@
 
 #include "tt_api.h"
 #include "tt_gemm_core.h"
+#include "tt_topk.h"
 
 namespace {
 
@@ -198,65 +199,7 @@ __global__ __launch_bounds__(256) void infonce_dscore_kernel(const T* __restrict
   });
 }
 
-// ------------------------------------------------------------- top-k (k <= 16)
-// One wave per row: lane-local sorted top-k over columns lane, lane+64, ...
-// (ascending scan, strict '>' insertion keeps the lower column first on ties),
-// then k rounds of a wave arg-max with (value desc, index asc) ordering.
-constexpr int TOPK_MAX = 16;
-__global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict__ S, long rows, long cols,
-                                                        long label_off, int k, int32_t* __restrict__ idx,
-                                                        float* __restrict__ val) {
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (row >= rows) return;
-  float lv[TOPK_MAX];
-  int li[TOPK_MAX];
-#pragma unroll
-  for (int q = 0; q < TOPK_MAX; ++q) { lv[q] = -FLT_MAX; li[q] = 0x7fffffff; }
-  const float* sr = S + row * cols;
-  const long lab = label_off >= 0 ? label_off + row : -1;  // label_off < 0: nothing masked
-  for (long c = lane; c < cols; c += 64) {
-    float v = sr[c];
-    if (c == lab) v = -1.f;
-    if (v > lv[k - 1]) {
-      // insert keeping descending order; equal values stay ahead (lower column)
-      float cv = v;
-      int ci = (int)c;
-#pragma unroll
-      for (int q = 0; q < TOPK_MAX; ++q) {
-        if (q < k && cv > lv[q]) {
-          const float tv = lv[q];
-          const int ti = li[q];
-          lv[q] = cv;
-          li[q] = ci;
-          cv = tv;
-          ci = ti;
-        }
-      }
-    }
-  }
-  int head = 0;
-  for (int q = 0; q < k; ++q) {
-    float hv = -FLT_MAX;
-    int hi = 0x7fffffff;
-#pragma unroll
-    for (int p = 0; p < TOPK_MAX; ++p)
-      if (p == head) { hv = lv[p]; hi = li[p]; }
-    float bv = hv;
-    int bi = hi;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(bv, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-    }
-    if (lane == 0) {
-      idx[row * k + q] = bi;
-      if (val) val[row * k + q] = bv;
-    }
-    if (hi == bi && head < TOPK_MAX) ++head;
-  }
-}
+constexpr int TOPK_MAX = ttk::SK_MAX;
 
 // ---------------------------------------------------------------- margin loss
 __global__ __launch_bounds__(256) void margin_fwd_kernel(const float* __restrict__ qn, long bq,
@@ -442,9 +385,11 @@ extern "C" int tt_infonce_bwd(int dtype, const void* qn, long bq, const void* dn
   return 0;
 }
 
+// ws: the score block S [bq, nd] fp32, then the per-chunk candidates (values, indices)
 extern "C" long tt_hardneg_ws_size(int dtype, long bq, long nd) {
   (void)dtype;
-  return bq * nd * 4;
+  const long ncand = tt_ceil_div(nd, ttk::split_chunk(bq, nd)) * (long)TOPK_MAX;
+  return ((bq * nd * 4 + 255) & ~255L) + 2 * ((bq * ncand * 4 + 255) & ~255L);
 }
 
 extern "C" int tt_hardneg_topk(int dtype, const void* qn, long bq, const void* dn, long nd, int h, long label_offset,
@@ -457,9 +402,26 @@ extern "C" int tt_hardneg_topk(int dtype, const void* qn, long bq, const void* d
   g.a[0] = qn; g.b[0] = dn; g.c[0] = S;
   TT_PROPAGATE(tt_gemm(dtype, TT_DT_F32, 0, 0, (int)bq, (int)nd, h, &g, 1, h, h, nd, 1.f, 0, 0, 0, 0, 0.f, 1,
                        nullptr, stream));
-  hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)tt_ceil_div(bq, 4)), dim3(256), 0, (hipStream_t)stream, S, bq,
-                     nd, label_offset, k, idx, val);
-  TT_CHECK_LAUNCH("topk_rows_kernel");
+  // many waves per row (column chunks), then one wave per row merges the candidates
+  const long chunk = ttk::split_chunk(bq, nd), nsp = tt_ceil_div(nd, chunk);
+  const long ncand = nsp * k;
+  char* cbase = static_cast<char*>(ws) + ((bq * nd * 4 + 255) & ~255L);
+  float* cv = reinterpret_cast<float*>(cbase);
+  int* ci = reinterpret_cast<int*>(cbase + ((bq * nsp * TOPK_MAX * 4 + 255) & ~255L));
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 gs((unsigned)tt_ceil_div(bq, 4), (unsigned)nsp);
+  if (k <= 4)
+    hipLaunchKernelGGL((ttk::topk_split_kernel<4>), gs, dim3(256), 0, st, S, bq, nd, chunk, label_offset, k, cv, ci);
+  else
+    hipLaunchKernelGGL((ttk::topk_split_kernel<TOPK_MAX>), gs, dim3(256), 0, st, S, bq, nd, chunk, label_offset, k,
+                       cv, ci);
+  TT_CHECK_LAUNCH("topk_split_kernel");
+  const dim3 gm((unsigned)tt_ceil_div(bq, 4));
+  if (k <= 4)
+    hipLaunchKernelGGL((ttk::topk_merge_kernel<4>), gm, dim3(256), 0, st, cv, ci, bq, ncand, k, idx, val);
+  else
+    hipLaunchKernelGGL((ttk::topk_merge_kernel<TOPK_MAX>), gm, dim3(256), 0, st, cv, ci, bq, ncand, k, idx, val);
+  TT_CHECK_LAUNCH("topk_merge_kernel");
   return 0;
 }
 

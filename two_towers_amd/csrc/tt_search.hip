@@ -7,73 +7,27 @@
 //     so they come through the scalar cache) and keeps a sorted per-lane top-k; each
 //     wave merges its lanes and writes k candidates; topk_merge_kernel reduces the
 //     candidates of all waves per query.
-//   larger Q: cosine GEMM into a score block, then topk_split_kernel (many waves per
-//     row, one column chunk each) and the same merge: the long rows of a large
-//     document pool are scanned by ceil(N / 4096) waves instead of one.
+//   larger Q: cosine GEMM into a score block, then ttk::topk_split_kernel (many waves
+//     per row, one column chunk each) and the same merge: the long rows of a large
+//     document pool are scanned by many waves instead of one.
 // Ordering everywhere: value descending, ties towards the lower document index.
 #include <cfloat>
 #include <climits>
 
 #include "tt_api.h"
 #include "tt_common.h"
+#include "tt_topk.h"
 
 namespace {
 
-constexpr int SK_MAX = 16;
+using ttk::SK_MAX;
+using ttk::insert;
+using ttk::wave_topk;
 // queries per scan workgroup: QB sorted lists of KM entries live in registers
 template <int KM> constexpr int scan_qb() { return KM <= 4 ? 8 : 2; }
 constexpr int SCAN_QMAX = 64;     // above this the GEMM path re-reads the matrix less
 constexpr int DOCS_PER_LANE = 4;  // 1024 documents per scan workgroup
 constexpr int BLK_DOCS = 256 * DOCS_PER_LANE;
-constexpr int SPLIT_COLS = 4096;  // columns per wave in topk_split_kernel
-
-TT_DEV bool better(float v, int i, float bv, int bi) { return v > bv || (v == bv && i < bi); }
-
-// Insert (v, id) into the descending list (lv, li)[0..k).
-template <int KM>
-TT_DEV void insert(float (&lv)[KM], int (&li)[KM], int k, float v, int id) {
-  if (!better(v, id, lv[k - 1], li[k - 1])) return;
-  float cv = v;
-  int ci = id;
-#pragma unroll
-  for (int q = 0; q < KM; ++q) {
-    if (q < k && better(cv, ci, lv[q], li[q])) {
-      const float tv = lv[q];
-      const int ti = li[q];
-      lv[q] = cv;
-      li[q] = ci;
-      cv = tv;
-      ci = ti;
-    }
-  }
-}
-
-// k rounds of a wave arg-max over the lanes' sorted lists; lane 0 gets the result.
-template <int KM>
-TT_DEV void wave_topk(const float (&lv)[KM], const int (&li)[KM], int k, float* ov, int* oi) {
-  const int lane = threadIdx.x & 63;
-  int head = 0;
-  for (int q = 0; q < k; ++q) {
-    float hv = -FLT_MAX;
-    int hi = INT_MAX;
-#pragma unroll
-    for (int p = 0; p < KM; ++p)
-      if (p == head) { hv = lv[p]; hi = li[p]; }
-    float bv = hv;
-    int bi = hi;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float xv = __shfl_xor(bv, o, 64);
-      const int xi = __shfl_xor(bi, o, 64);
-      if (better(xv, xi, bv, bi)) { bv = xv; bi = xi; }
-    }
-    if (lane == 0) {
-      ov[q] = bv;
-      oi[q] = bi;
-    }
-    if (hi == bi && head < KM) ++head;
-  }
-}
 
 template <typename T, int KM, int SCAN_QB = scan_qb<KM>()>
 __global__ __launch_bounds__(256) void search_scan_kernel(const float* __restrict__ qn, long Q,
@@ -87,9 +41,7 @@ __global__ __launch_bounds__(256) void search_scan_kernel(const float* __restric
   float lv[SCAN_QB][KM];
   int li[SCAN_QB][KM];
 #pragma unroll
-  for (int q = 0; q < SCAN_QB; ++q)
-#pragma unroll
-    for (int j = 0; j < KM; ++j) { lv[q][j] = -FLT_MAX; li[q][j] = INT_MAX; }
+  for (int q = 0; q < SCAN_QB; ++q) ttk::init<KM>(lv[q], li[q]);
   const long dbase = (long)blockIdx.x * BLK_DOCS + wave * 64 * DOCS_PER_LANE + lane;
   for (int r = 0; r < DOCS_PER_LANE; ++r) {
     const long d = dbase + 64L * r;
@@ -124,49 +76,6 @@ __global__ __launch_bounds__(256) void search_scan_kernel(const float* __restric
   }
 }
 
-// One wave per (row, column chunk) of a dense score block S [rows, cols].
-template <int KM>
-__global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict__ S, long rows, long cols,
-                                                         int k, float* __restrict__ cv, int* __restrict__ ci) {
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (row >= rows) return;
-  float lv[KM];
-  int li[KM];
-#pragma unroll
-  for (int j = 0; j < KM; ++j) { lv[j] = -FLT_MAX; li[j] = INT_MAX; }
-  const long c0 = (long)blockIdx.y * SPLIT_COLS;
-  const long c1 = c0 + SPLIT_COLS < cols ? c0 + SPLIT_COLS : cols;
-  const float* sr = S + row * cols;
-  for (long c = c0 + lane; c < c1; c += 64) insert<KM>(lv, li, k, sr[c], (int)c);
-  const long o = (row * gridDim.y + blockIdx.y) * k;
-  wave_topk<KM>(lv, li, k, cv + o, ci + o);
-}
-
-// One wave per row: top-k of ncand candidates (cv, ci)[row][0..ncand).
-template <int KM>
-__global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict__ cv, const int* __restrict__ ci,
-                                                         long rows, long ncand, int k, int32_t* __restrict__ idx,
-                                                         float* __restrict__ val) {
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (row >= rows) return;
-  float lv[KM];
-  int li[KM];
-#pragma unroll
-  for (int j = 0; j < KM; ++j) { lv[j] = -FLT_MAX; li[j] = INT_MAX; }
-  for (long c = lane; c < ncand; c += 64) insert<KM>(lv, li, k, cv[row * ncand + c], ci[row * ncand + c]);
-  float ov[KM];
-  int oi[KM];
-  wave_topk<KM>(lv, li, k, ov, oi);
-  if (lane == 0) {
-    for (int q = 0; q < k; ++q) {
-      idx[row * k + q] = oi[q];
-      if (val) val[row * k + q] = ov[q];
-    }
-  }
-}
-
 struct SearchWs {
   long cv, ci, qd, S, total;
 };
@@ -179,7 +88,7 @@ inline SearchWs search_ws(int dtype, long Q, long N, int h, int k) {
     ncand = tt_ceil_div(N, BLK_DOCS) * 4 * k;
     w.qd = w.S = 0;
   } else {
-    ncand = tt_ceil_div(N, SPLIT_COLS) * k;
+    ncand = tt_ceil_div(N, ttk::split_chunk(Q, N)) * k;
   }
   w.cv = off; off = al(off + Q * ncand * 4);
   w.ci = off; off = al(off + Q * ncand * 4);
@@ -219,13 +128,13 @@ int search_launch(int dtype, const float* qn, long Q, const void* dn, long N, in
     g.a[0] = qd; g.b[0] = dn; g.c[0] = S;
     TT_PROPAGATE(tt_gemm(dtype, TT_DT_F32, 0, 0, (int)Q, (int)N, h, &g, 1, h, h, N, 1.f, 0, 0, 0, 0, 0.f, 1, nullptr,
                          st));
-    const long nsp = tt_ceil_div(N, SPLIT_COLS);
+    const long chunk = ttk::split_chunk(Q, N), nsp = tt_ceil_div(N, chunk);
     ncand = nsp * k;
-    hipLaunchKernelGGL((topk_split_kernel<KM>), dim3((unsigned)tt_ceil_div(Q, 4), (unsigned)nsp), dim3(256), 0, st,
-                       S, Q, N, k, cv, ci);
+    hipLaunchKernelGGL((ttk::topk_split_kernel<KM>), dim3((unsigned)tt_ceil_div(Q, 4), (unsigned)nsp), dim3(256), 0,
+                       st, S, Q, N, chunk, -1L, k, cv, ci);
     TT_CHECK_LAUNCH("topk_split_kernel");
   }
-  hipLaunchKernelGGL((topk_merge_kernel<KM>), dim3((unsigned)tt_ceil_div(Q, 4)), dim3(256), 0, st, cv, ci, Q, ncand,
+  hipLaunchKernelGGL((ttk::topk_merge_kernel<KM>), dim3((unsigned)tt_ceil_div(Q, 4)), dim3(256), 0, st, cv, ci, Q, ncand,
                      k, idx, val);
   TT_CHECK_LAUNCH("topk_merge_kernel");
   return 0;

@@ -238,10 +238,12 @@ long tt_infonce_bwd_ws_size(int dtype, long bq, long nd, int h);
  * (1 <= k <= min(16, nd)) indices per row sorted by descending similarity; ties broken
  * towards the lower column index. Also the scoring step of the serving /search
  * (server/python-api/app.py:94-101, label_offset < 0).
- * idx [bq, k] int32, val [bq, k] fp32 (optional). ws: tt_hardneg_ws_size bytes. */
+ * idx [bq, k] int32, val [bq, k] fp32 (optional). ws: tt_hardneg_ws_size bytes.
+ * bf16 with h in {128, 256} (qn, dn 16-byte aligned, else TT_EINVAL) never stores the score matrix
+ * (streamed MFMA scan + exact chunk selection + bit-identical rescoring, tt_score.hip). */
 int tt_hardneg_topk(int dtype, const void* qn, long bq, const void* dn, long nd, int h,
                     long label_offset, int k, int32_t* idx, float* val, void* ws, void* stream);
-long tt_hardneg_ws_size(int dtype, long bq, long nd);
+long tt_hardneg_ws_size(int dtype, long bq, long nd, int h, int k);
 
 /* Serving search (server/python-api/app.py:94-101: F.cosine_similarity of one encoded
  * query against every cached document row, then torch.topk): qn [Q, h] fp32 normalised

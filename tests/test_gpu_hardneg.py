@@ -1,0 +1,118 @@
+"""tt_hardneg_topk (get_hard_negatives, enhanced_two_tower.py:123-133, batched) through the
+C ABI. bf16 with h in {128, 256} runs the streamed scan of tt_score.hip (chunk maxima ->
+exact chunk selection -> bit-identical rescoring -> top-k); other shapes run the GEMM +
+split top-k of tt_loss.hip. Integer-valued operands make every dot product exact in fp32
+whatever the summation order, so indices -- ties included, which go to the lower column
+-- and values are compared bit-exactly against a float64 reference of the reference rule
+(positive column set to -1, then topk)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from two_towers_amd import _lib  # noqa: E402
+from two_towers_amd._lib import call, dtype_code  # noqa: E402
+
+DEV = "cuda"
+
+
+def ref_hardneg(q, d, label_offset, k):
+    s = (q.double() @ d.double().t()).cpu()
+    if label_offset >= 0:
+        rows = torch.arange(q.shape[0])
+        s[rows, label_offset + rows] = -1.0
+    # stable sort by (-value, index)
+    order = torch.sort(-s, dim=1, stable=True).indices[:, :k]
+    return order, torch.gather(s, 1, order)
+
+
+def run_hardneg(q, d, label_offset, k, dt):
+    lib = _lib.load()
+    B, h = q.shape
+    nd = d.shape[0]
+    qd, dd = q.to(DEV, dt).contiguous(), d.to(DEV, dt).contiguous()
+    idx = torch.empty(B, k, dtype=torch.int32, device=DEV)
+    val = torch.empty(B, k, dtype=torch.float32, device=DEV)
+    ws = torch.empty(max(lib.tt_hardneg_ws_size(dtype_code(dt), B, nd, h, k), 1), dtype=torch.uint8, device=DEV)
+    call("tt_hardneg_topk", dtype_code(dt), qd.data_ptr(), B, dd.data_ptr(), nd, h, label_offset, k, idx.data_ptr(),
+         val.data_ptr(), ws.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return idx.cpu().long(), val.cpu()
+
+
+CASES = [  # B, nd, h, label_offset, k
+    (300, 1000, 256, 0, 5),      # labels on the diagonal, nd not a multiple of 64
+    (513, 513, 256, 0, 5),       # B = nd, partial row tile and partial chunk
+    (64, 4096, 256, 1024, 5),    # label offset (DP rank 1 of 4)
+    (257, 2000, 128, -1, 16),    # nothing masked (serving), k = 16
+    (100, 200, 256, 0, 5),       # nch = 4 < k: every chunk selected
+    (40, 70, 128, 3, 1),         # k = 1, two chunks
+    (96, 640, 64, 0, 5),         # GEMM + split path (h = 64)
+    (33, 999, 96, -1, 7),        # GEMM + split path (h = 96)
+]
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("B,nd,h,lab,k", CASES)
+def test_hardneg_exact(dt, B, nd, h, lab, k):
+    g = torch.Generator().manual_seed(B * 7919 + nd * 31 + h)
+    q = torch.randint(-3, 4, (B, h), generator=g).float()
+    d = torch.randint(-3, 4, (nd, h), generator=g).float()
+    d[nd // 2] = d[nd // 3]          # exact ties across chunks: lower index first
+    d[nd - 1] = d[5]
+    if nd > 130:
+        d[70] = d[129]               # a tie inside neighbouring chunks
+    ri, rv = ref_hardneg(q, d, lab, k)
+    gi, gv = run_hardneg(q, d, lab, k, dt)
+    assert torch.equal(gi, ri)
+    assert torch.equal(gv.double(), rv)
+
+
+@pytest.mark.parametrize("h", [128, 256])
+def test_hardneg_all_ties(h):
+    """Every score equal: all chunk maxima tie, so the selection must take the lowest
+    chunks and the result is the k lowest unmasked columns."""
+    B, nd, k = 70, 900, 5
+    q = torch.ones(B, h)
+    d = torch.ones(nd, h)
+    ri, rv = ref_hardneg(q, d, 0, k)
+    gi, gv = run_hardneg(q, d, 0, k, torch.bfloat16)
+    assert torch.equal(gi, ri)
+    assert torch.equal(gv.double(), rv)
+
+
+def test_hardneg_bench_size_consistent():
+    """bench shape (8192 x 8192, h 256, bf16, normalised rows): the returned values are
+    the float64 scores of the returned columns (to fp32 MFMA rounding), sorted, and no
+    column outside the result scores more than the k-th result."""
+    B, nd, h, k = 8192, 8192, 256, 5
+    g = torch.Generator().manual_seed(11)
+    q = torch.nn.functional.normalize(torch.randn(B, h, generator=g), dim=1).bfloat16().float()
+    d = torch.nn.functional.normalize(torch.randn(nd, h, generator=g), dim=1).bfloat16().float()
+    gi, gv = run_hardneg(q, d, 0, k, torch.bfloat16)
+    s = (q.to(DEV).double() @ d.to(DEV).double().t())
+    rows = torch.arange(B, device=DEV)
+    s[rows, rows] = -1.0
+    gi_d = gi.to(DEV)
+    got = torch.gather(s, 1, gi_d)
+    assert (got.cpu() - gv.double()).abs().max() < 1e-5
+    assert bool((gv[:, :-1] >= gv[:, 1:]).all())
+    s.scatter_(1, gi_d, -2.0)
+    assert bool((s.max(dim=1).values.cpu() <= gv[:, -1].double() + 1e-5).all())
+    assert len(set(gi[0].tolist())) == k
+
+
+@pytest.mark.parametrize("B,nd,h,lab", [(1000, 3000, 256, 0), (300, 4100, 128, -1), (8192, 8192, 256, 0)])
+def test_hardneg_scan_matches_gemm_path(monkeypatch, B, nd, h, lab):
+    """Random (non-integer) normalised bf16 rows: the streamed scan and the GEMM + split
+    top-k path form every score with the same MFMA instruction and k order, so indices
+    and values agree bit-exactly -- including near-ties, which a rescoring that differed
+    from the scan's arithmetic by one ulp would flip."""
+    g = torch.Generator().manual_seed(B + nd + h)
+    q = torch.nn.functional.normalize(torch.randn(B, h, generator=g), dim=1)
+    d = torch.nn.functional.normalize(torch.randn(nd, h, generator=g), dim=1)
+    si, sv = run_hardneg(q, d, lab, 5, torch.bfloat16)
+    monkeypatch.setenv("TT_HN_GEMM", "1")
+    gi, gv = run_hardneg(q, d, lab, 5, torch.bfloat16)
+    assert torch.equal(sv, gv)
+    assert torch.equal(si, gi)

@@ -1,0 +1,73 @@
+"""Micro-benchmark of the score-matrix kernels at the bench shapes (HIP-event timed on
+the launching stream): hard-negative mining (tt_hardneg_topk) and the fused InfoNCE
+forward. Run under `rocprofv3 --kernel-trace --stats` for the per-kernel split."""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from two_towers_amd import _lib  # noqa: E402
+from two_towers_amd._lib import call, dtype_code  # noqa: E402
+
+
+def timed(f, iters):
+    f()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        f()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def hardneg(B, nd, h, k, dt, iters):
+    lib = _lib.load()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    q = torch.nn.functional.normalize(torch.randn(B, h, device="cuda", generator=g), dim=1).to(dt)
+    d = torch.nn.functional.normalize(torch.randn(nd, h, device="cuda", generator=g), dim=1).to(dt)
+    idx = torch.empty(B, k, dtype=torch.int32, device="cuda")
+    ws = torch.empty(lib.tt_hardneg_ws_size(dtype_code(dt), B, nd, h, k), dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    f = lambda: call("tt_hardneg_topk", dtype_code(dt), q.data_ptr(), B, d.data_ptr(), nd, h, 0, k, idx.data_ptr(),
+                     None, ws.data_ptr(), st)
+    ms = timed(f, iters)
+    tf = 2.0 * B * nd * h / (ms * 1e-3) / 1e12
+    return {"op": "hardneg_topk", "B": B, "nd": nd, "h": h, "k": k, "dtype": str(dt)[6:], "ms": round(ms, 4),
+            "tflops": round(tf, 1), "mfma_frac": round(tf / 2500.0, 4)}
+
+
+def infonce(B, nd, h, dt, iters):
+    lib = _lib.load()
+    g = torch.Generator(device="cuda").manual_seed(6)
+    q = torch.nn.functional.normalize(torch.randn(B, h, device="cuda", generator=g), dim=1).to(dt)
+    d = torch.nn.functional.normalize(torch.randn(nd, h, device="cuda", generator=g), dim=1).to(dt)
+    lse = torch.empty(B, device="cuda")
+    rl = torch.empty(B, device="cuda")
+    ws = torch.empty(max(lib.tt_infonce_fwd_ws_size(B, nd), 1), dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    f = lambda: call("tt_infonce_fwd", dtype_code(dt), q.data_ptr(), B, d.data_ptr(), nd, h, 1.0 / 0.07, 0.0, 0,
+                     lse.data_ptr(), rl.data_ptr(), ws.data_ptr(), st)
+    ms = timed(f, iters)
+    tf = 2.0 * B * nd * h / (ms * 1e-3) / 1e12
+    return {"op": "infonce_fwd", "B": B, "nd": nd, "h": h, "dtype": str(dt)[6:], "ms": round(ms, 4),
+            "tflops": round(tf, 1), "mfma_frac": round(tf / 2500.0, 4)}
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--ops", default="hardneg,infonce")
+    a = ap.parse_args()
+    bf = torch.bfloat16
+    if "hardneg" in a.ops:
+        for B, nd in ((8192, 8192), (8192, 65536)):
+            print(json.dumps(hardneg(B, nd, 256, 5, bf, a.iters)), flush=True)
+        print(json.dumps(hardneg(8192, 8192, 512, 5, bf, a.iters)), flush=True)
+    if "infonce" in a.ops:
+        for B, nd, h in ((8192, 8192, 256), (8192, 65536, 256), (8192, 8192, 512)):
+            print(json.dumps(infonce(B, nd, h, bf, a.iters)), flush=True)

@@ -119,7 +119,7 @@ _SIGS = {
     "tt_infonce_bwd_ws_size": (c_long, [c_int, c_long, c_long, c_int]),
     "tt_hardneg_topk": (c_int, [c_int, c_void_p, c_long, c_void_p, c_long, c_int, c_long, c_int, c_void_p,
                                 c_void_p, c_void_p, c_void_p]),
-    "tt_hardneg_ws_size": (c_long, [c_int, c_long, c_long]),
+    "tt_hardneg_ws_size": (c_long, [c_int, c_long, c_long, c_int, c_int]),
     "tt_search_topk": (c_int, [c_int, c_void_p, c_long, c_void_p, c_long, c_int, c_int, c_void_p, c_void_p,
                                c_void_p, c_void_p]),
     "tt_search_ws_size": (c_long, [c_int, c_long, c_long, c_int, c_int]),

@@ -386,8 +386,14 @@ extern "C" int tt_infonce_bwd(int dtype, const void* qn, long bq, const void* dn
 }
 
 // ws: the score block S [bq, nd] fp32, then the per-chunk candidates (values, indices)
-extern "C" long tt_hardneg_ws_size(int dtype, long bq, long nd) {
-  (void)dtype;
+// bf16 operands with h in {128, 256}: the streamed scan of tt_score.hip (no score matrix)
+long tt_hn_scan_ws_size(long bq, long nd, int k);
+bool tt_hn_scan_supported(int dtype, int h);
+int tt_hn_scan_topk(const void* qn, long bq, const void* dn, long nd, int h, long label_offset, int k, int32_t* idx,
+                    float* val, void* ws, void* stream);
+
+extern "C" long tt_hardneg_ws_size(int dtype, long bq, long nd, int h, int k) {
+  if (tt_hn_scan_supported(dtype, h)) return tt_hn_scan_ws_size(bq, nd, k < 1 ? 1 : k);
   const long ncand = tt_ceil_div(nd, ttk::split_chunk(bq, nd)) * (long)TOPK_MAX;
   return ((bq * nd * 4 + 255) & ~255L) + 2 * ((bq * ncand * 4 + 255) & ~255L);
 }
@@ -397,6 +403,10 @@ extern "C" int tt_hardneg_topk(int dtype, const void* qn, long bq, const void* d
   TT_CHECK_ARG(k >= 1 && k <= TOPK_MAX && k <= nd, "tt_hardneg_topk: k=%d (nd=%ld)", k, nd);
   TT_CHECK_ARG(label_offset < 0 || label_offset + bq <= nd, "tt_hardneg_topk: labels outside [0, nd)");
   if (bq == 0) return 0;
+  if (tt_hn_scan_supported(dtype, h)) {
+    TT_CHECK_ARG((((uintptr_t)qn | (uintptr_t)dn) & 15) == 0, "tt_hardneg_topk: bf16 rows must be 16-byte aligned");
+    return tt_hn_scan_topk(qn, bq, dn, nd, h, label_offset, k, idx, val, ws, stream);
+  }
   float* S = static_cast<float*>(ws);
   tt_gemm_batch g{};
   g.a[0] = qn; g.b[0] = dn; g.c[0] = S;

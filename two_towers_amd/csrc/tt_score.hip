@@ -1,0 +1,462 @@
+// Score-matrix scans on MFMA that never store the B x N score matrix.
+//
+// Hard-negative mining (get_hard_negatives, enhanced_two_tower.py:123-133, batched over
+// rows; the positive column scores -1, enhanced_two_tower.py:130) as an exact top-k in
+// four launches:
+//   1. hn_scan    : S = Q D^T on MFMA, streamed: one workgroup keeps 256 query rows in
+//                   registers and sweeps 64-column document tiles through a 3-slot LDS
+//                   ring (LDS-DMA, two tiles in flight). Per (row, 64-column chunk) it
+//                   keeps only the chunk maximum.
+//   2. hn_select  : per row, the k chunks ranked first by (chunk max desc, chunk asc).
+//                   Every element of the row's top-k lies in them: the k-th chunk max
+//                   theta is a value with >= k elements at or above it, so each top-k
+//                   element is >= theta, and lives in a chunk whose max is > theta (all of
+//                   those are selected) or == theta (the lowest-indexed of those are
+//                   selected, and they hold the lowest-indexed elements equal to theta).
+//   3. hn_rescore : per chunk, the rows that selected it (gathered 16 at a time) x the
+//                   chunk's 64 columns recomputed with
+//                   the SAME MFMA sequence as step 1 (same instruction, same k order, same
+//                   fragment k layout), so each score is bit-identical to the one step 1
+//                   ranked; k x 64 candidates per row.
+//   4. hn_final   : per row, top-k of its candidates (value desc, column asc).
+// Work: step 1 is the whole contraction (2 B N h FLOPs); steps 2-4 touch B k 64 h.
+#include <float.h>
+#include <stdlib.h>
+
+#include "tt_api.h"
+#include "tt_gemm_core.h"
+#include "tt_topk.h"
+
+namespace {
+
+constexpr int SC_COLS = 64;                     // document columns per tile (= per chunk)
+constexpr int SC_WAVES = 8;                     // 512 threads: two waves per SIMD
+constexpr int SC_RB = 2;                        // 16-query MFMA blocks per wave
+constexpr int SC_ROWS = SC_WAVES * SC_RB * 16;  // 256 query rows per workgroup
+constexpr int SC_TPS_MAX = 32;                  // tiles per workgroup (chunk-max staging)
+constexpr int SC_SLOTS = 4;                     // LDS tile ring: two pairs of tiles
+
+// max over the four 16-lane rows of a wave (lanes l, l+16, l+32, l+48), result in all
+TT_DEV float rowgroup_max4(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+// LDS image of one 64-column document tile, h = 32 KS bf16 per document: document n
+// holds CPR 16-byte chunks, chunk c stored at slot c ^ (n & 15) so that the fragment
+// reads (16 documents x one chunk per lane group) are bank-conflict free.
+template <int KS>
+struct ScanTile {
+  static constexpr int CPR = KS * 4;
+  static constexpr int BYTES = SC_COLS * CPR * 16;
+  static constexpr int DPW = BYTES / 1024 / SC_WAVES;  // 1 KiB DMA instructions per wave
+  static_assert(DPW >= 1 && BYTES % (1024 * SC_WAVES) == 0, "tile/wave mismatch");
+  TT_DEV static int off(int n, int c) { return (n * CPR + (c ^ (n & 15))) * 16; }
+};
+
+// One lane's share of a tile DMA, resolved once: element offset within the tile and the
+// tile document it reads.
+template <int KS>
+struct ScanDma {
+  using TI = ScanTile<KS>;
+  int doc[TI::DPW];
+  int eoff[TI::DPW];
+  TT_DEV void init() {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < TI::DPW; ++i) {
+      const int p = (wave * TI::DPW + i) * 64 + lane;
+      const int n = p / TI::CPR, c = (p % TI::CPR) ^ (n & 15);
+      doc[i] = n;
+      eoff[i] = n * (32 * KS) + c * 8;
+    }
+  }
+  TT_DEV void issue(const bf16_t* __restrict__ D, long nd, long n0, uint32_t base) const {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bf16_t* tb = D + n0 * (32 * KS);
+#pragma unroll
+    for (int i = 0; i < TI::DPW; ++i) {
+      const void* src = n0 + doc[i] < nd ? static_cast<const void*>(tb + eoff[i]) : ttg::g_tt_zero_page;
+      ttg::dma16(src, __builtin_amdgcn_readfirstlane(base + (uint32_t)(wave * TI::DPW + i) * 1024u));
+    }
+  }
+};
+
+// Fragment of row `row` of a [nrows, 32 KS] bf16 matrix for k-step ks: lane holds
+// elements k = 32 ks + 8 (lane >> 4) .. +8 (the 16x16x32 operand layout).
+TT_DEV uint4 ld_frag(const bf16_t* __restrict__ base, long row, long nrows, int h, int ks) {
+  const int lane = threadIdx.x & 63;
+  if (row >= nrows) return make_uint4(0, 0, 0, 0);
+  return *reinterpret_cast<const uint4*>(base + row * h + ks * 32 + 8 * (lane >> 4));
+}
+
+// Step 1. The MFMA runs transposed, C[doc][query] = sum_k D[doc][k] Q[query][k]: A = the
+// LDS document fragments, B = the register-resident query fragments (both operands use
+// the same 16-rows x 8-k per lane layout). So each lane holds 16 scores of ONE query per
+// 64-document tile and the chunk maximum is 15 lane-local max + two permlane swaps.
+// Grid: row tiles x column splits, 1-D: block b -> split b % S (a split's workgroups
+// share one XCD label and its document slice stays in that L2), row tile b / S.
+template <int KS>
+__global__ __launch_bounds__(SC_WAVES * 64, 1) void hn_scan_kernel(const bf16_t* __restrict__ Q, long bq,
+                                                                 const bf16_t* __restrict__ D, long nd,
+                                                                 long label_off, int S, int tps, long nch,
+                                                                 float* __restrict__ CM) {
+  using TI = ScanTile<KS>;
+  // 4 x 32 KiB tile ring + chunk maxima [tile][row]: all 160 KiB, one workgroup per CU
+  __shared__ __attribute__((aligned(16))) char lds[SC_SLOTS * TI::BYTES + SC_TPS_MAX * SC_ROWS * 4];
+  float* cms = reinterpret_cast<float*>(lds + SC_SLOTS * TI::BYTES);
+  const int split = blockIdx.x % S, rt = blockIdx.x / S;
+  const long t0 = (long)split * tps;
+  const int nt = (int)(nch - t0 < tps ? nch - t0 : tps);
+  if (nt <= 0) return;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const long row0 = (long)rt * SC_ROWS + wave * (SC_RB * 16);
+  constexpr int h = 32 * KS;
+  // The first two tiles are requested before the query rows, so their latency overlaps.
+  ScanDma<KS> dm;
+  dm.init();
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane(ttg::lds_addr_of(lds));
+  dm.issue(D, nd, t0 * SC_COLS, lbase);
+  if (nt > 1) dm.issue(D, nd, (t0 + 1) * SC_COLS, lbase + TI::BYTES);
+  uint4 qa[SC_RB][KS];
+#pragma unroll
+  for (int qb = 0; qb < SC_RB; ++qb)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qa[qb][ks] = ld_frag(Q, row0 + qb * 16 + (lane & 15), bq, h, ks);
+  // Retire the query loads here, so that hipcc does not place a vmcnt(0) inside the tile
+  // loop (it cannot see the LDS-DMAs and would wait for the tiles in flight every tile).
+#pragma unroll
+  for (int qb = 0; qb < SC_RB; ++qb)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      asm volatile("" ::"v"(qa[qb][ks].x), "v"(qa[qb][ks].y), "v"(qa[qb][ks].z), "v"(qa[qb][ks].w));
+
+  // Tiles travel in pairs: at every even tile, one wait + barrier retires the pair (t, t+1)
+  // for every wave and frees slots (t+2)%4, (t+3)%4 (last read before this barrier), into
+  // which the next pair is requested; it lands while this pair is computed.
+  auto sync = [&](int t) {
+    if ((t & 1) == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (t + 2 < nt) dm.issue(D, nd, (t0 + t + 2) * SC_COLS, lbase + (uint32_t)((t + 2) % SC_SLOTS) * TI::BYTES);
+      if (t + 3 < nt) dm.issue(D, nd, (t0 + t + 3) * SC_COLS, lbase + (uint32_t)((t + 3) % SC_SLOTS) * TI::BYTES);
+    }
+  };
+  // Chunk maxima of tile t (masked form: positive -> -1, documents past nd -> -inf).
+  auto chunk_max = [&](const f32x4 (&a)[4][SC_RB], int t, bool masked) {
+    const int n0 = (int)((t0 + t) * SC_COLS);
+    const bool diag = label_off >= 0 && label_off + row0 < n0 + SC_COLS && n0 < label_off + row0 + SC_RB * 16;
+#pragma unroll
+    for (int qb = 0; qb < SC_RB; ++qb) {
+      float v[16];
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[db * 4 + r] = a[db][qb][r];
+      if (masked) {
+        const int lab = (int)(label_off + row0) + qb * 16 + (lane & 15) - n0;  // tile-relative
+        const int lim = (int)(nd - n0);
+#pragma unroll
+        for (int db = 0; db < 4; ++db)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int doc = db * 16 + 4 * (lane >> 4) + r;
+            if (diag && doc == lab) v[db * 4 + r] = -1.f;
+            if (doc >= lim) v[db * 4 + r] = -FLT_MAX;
+          }
+      }
+      float m = fmaxf(fmaxf(v[0], v[1]), v[2]);
+#pragma unroll
+      for (int j = 3; j < 15; j += 2) m = fmaxf(fmaxf(m, v[j]), v[j + 1]);
+      m = rowgroup_max4(fmaxf(m, v[15]));
+      if (lane < 16) cms[t * SC_ROWS + wave * SC_RB * 16 + qb * 16 + lane] = m;
+    }
+  };
+  // MFMAs of tile t into acc, with (EPI) the unmasked chunk maxima of tile t-1 (prev)
+  // woven between its k-steps. Program order is pinned with sched_barrier: per k-step,
+  // the fragment reads of k-step ks+2, the 8 MFMAs of ks, then one slice of the epilogue,
+  // so the LDS reads run two k-steps ahead and the epilogue VALU fills MFMA issue gaps
+  // (hipcc otherwise sinks every read to just before its MFMA and clusters the VALU).
+  auto tile = [&](f32x4 (&acc)[4][SC_RB], const f32x4 (&prev)[4][SC_RB], int t, bool epi) {
+    const char* img = lds + (t % SC_SLOTS) * TI::BYTES;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int qb = 0; qb < SC_RB; ++qb) acc[db][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint4 fa[3][4];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+        fa[ks][db] = *reinterpret_cast<const uint4*>(img + TI::off(db * 16 + (lane & 15), ks * 4 + (lane >> 4)));
+    // epilogue slice i: query block i / 3; two half-maxima (documents 0-31, 32-63), then
+    // the 4-row-group reduction and the store
+    float m = 0.f;
+    auto slice = [&](int i) {
+      const int qb = i / 3, part = i % 3;
+      if (qb >= SC_RB) return;
+      if (part < 2) {
+        const f32x4 x = prev[2 * part][qb], y = prev[2 * part + 1][qb];
+        const float hm =
+            fmaxf(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])), fmaxf(fmaxf(y[0], y[1]), fmaxf(y[2], y[3])));
+        m = part == 0 ? hm : fmaxf(m, hm);
+      } else {
+        m = rowgroup_max4(m);
+        if (lane < 16) cms[(t - 1) * SC_ROWS + wave * SC_RB * 16 + qb * 16 + lane] = m;
+      }
+    };
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 2 < KS) {
+#pragma unroll
+        for (int db = 0; db < 4; ++db)
+          fa[(ks + 2) % 3][db] =
+              *reinterpret_cast<const uint4*>(img + TI::off(db * 16 + (lane & 15), (ks + 2) * 4 + (lane >> 4)));
+      }
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int qb = 0; qb < SC_RB; ++qb)
+          acc[db][qb] = ttg::mma<bf16_t>(fa[ks % 3][db], qa[qb][ks], acc[db][qb]);
+      if (epi) slice(ks);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (epi) {
+#pragma unroll
+      for (int i = KS; i < 3 * SC_RB; ++i) slice(i);
+    }
+  };
+  f32x4 accA[4][SC_RB], accB[4][SC_RB];
+  // Tiles holding a positive (label) column or documents past nd take the masked form.
+  auto special = [&](int t) {
+    const long n0 = (t0 + t) * SC_COLS;
+    return (label_off >= 0 && label_off + row0 < n0 + SC_COLS && n0 < label_off + row0 + SC_RB * 16) ||
+           n0 + SC_COLS > nd;
+  };
+  auto step = [&](f32x4 (&cur)[4][SC_RB], const f32x4 (&prev)[4][SC_RB], int t) {  // t >= 1
+    sync(t);
+    if (special(t - 1)) {
+      tile(cur, prev, t, false);
+      chunk_max(prev, t - 1, true);
+    } else {
+      tile(cur, prev, t, true);
+    }
+  };
+  sync(0);
+  tile(accB, accA, 0, false);
+  int t = 1;
+  for (; t + 1 < nt; t += 2) {
+    step(accA, accB, t);
+    step(accB, accA, t + 1);
+  }
+  if (t < nt) {
+    step(accA, accB, t);
+    chunk_max(accA, t, special(t));
+  } else {
+    chunk_max(accB, t - 1, special(t - 1));
+  }
+  __syncthreads();
+  const long rbase = (long)rt * SC_ROWS;
+  for (int e = threadIdx.x; e < SC_ROWS * nt; e += SC_WAVES * 64) {
+    const int rl = e / nt, tt = e % nt;
+    if (rbase + rl < bq) CM[(rbase + rl) * nch + t0 + tt] = cms[tt * SC_ROWS + rl];
+  }
+}
+
+// Step 2: one wave per row: sel[row][0..nsel) = the chunks ranked first.
+template <int KM>
+__global__ __launch_bounds__(256) void hn_select_kernel(const float* __restrict__ CM, long bq, long nch, int k,
+                                                        int32_t* __restrict__ sel) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= bq) return;
+  float lv[KM];
+  int li[KM];
+  ttk::init<KM>(lv, li);
+  const int nsel = (int)(nch < k ? nch : k);
+  for (long c = lane; c < nch; c += 64) ttk::insert<KM>(lv, li, nsel, CM[row * nch + c], (int)c);
+  float ov[KM];
+  int oi[KM];
+  ttk::wave_topk<KM>(lv, li, nsel, ov, oi);
+  if (lane == 0)
+    for (int q = 0; q < nsel; ++q) sel[row * k + q] = oi[q];
+}
+
+// Step 3: one workgroup per chunk c. It collects the (row, slot) entries that selected c
+// (a scan of sel; LDS list), then its waves rescore them 16 rows at a time with the
+// MFMA orientation and k order of step 1: the chunk's documents as A (registers), the
+// gathered query rows as B.
+constexpr int RS_LIST = 8192;
+constexpr int RS_THREADS = 512;
+
+template <int KS>
+__global__ __launch_bounds__(RS_THREADS) void hn_rescore_kernel(const bf16_t* __restrict__ Q, long bq,
+                                                         const bf16_t* __restrict__ D, long nd, long label_off, int k,
+                                                         int nsel, const int32_t* __restrict__ sel,
+                                                         float* __restrict__ cand) {
+  constexpr int h = 32 * KS;
+  __shared__ int list[RS_LIST];
+  __shared__ int lcount;
+  const int c = blockIdx.x;
+  const long n0 = (long)c * SC_COLS;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint4 fa[4][KS];
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) fa[db][ks] = ld_frag(D, n0 + db * 16 + (lane & 15), nd, h, ks);
+  for (long seg = 0; seg < bq; seg += RS_LIST) {  // a row selects a chunk at most once
+    const long seg1 = seg + RS_LIST < bq ? seg + RS_LIST : bq;
+    if (threadIdx.x == 0) lcount = 0;
+    __syncthreads();
+    // the segment's entries, 4 per 16-byte load, several loads in flight per thread
+    const int total = (int)(seg1 - seg) * k;
+    const int4* s4 = reinterpret_cast<const int4*>(sel + seg * k);
+#pragma unroll 4
+    for (int i = threadIdx.x; i < total / 4; i += RS_THREADS) {
+      const int4 v = s4[i];
+      const int w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (w[j] == c && (nsel == k || (4 * i + j) % k < nsel)) list[atomicAdd(&lcount, 1)] = 4 * i + j;
+    }
+    for (int e = total / 4 * 4 + threadIdx.x; e < total; e += RS_THREADS)
+      if (sel[seg * k + e] == c && (nsel == k || e % k < nsel)) list[atomicAdd(&lcount, 1)] = e;
+    __syncthreads();
+    const int n = lcount;
+    for (int g = wave; g * 16 < n; g += RS_THREADS / 64) {
+      const int ei = g * 16 + (lane & 15);
+      const long e = ei < n ? seg * k + list[ei] : -1;
+      const long row = e >= 0 ? e / k : bq;  // bq -> zero fragment
+      f32x4 acc[4];
+#pragma unroll
+      for (int db = 0; db < 4; ++db) acc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const uint4 qf = ld_frag(Q, row, bq, h, ks);
+#pragma unroll
+        for (int db = 0; db < 4; ++db) acc[db] = ttg::mma<bf16_t>(fa[db][ks], qf, acc[db]);
+      }
+      if (e >= 0) {
+        float* dst = cand + e * SC_COLS;  // e = row * k + slot
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const long doc = n0 + db * 16 + 4 * (lane >> 4) + r;
+            v[r] = acc[db][r];
+            if (label_off >= 0 && doc == label_off + row) v[r] = -1.f;
+            if (doc >= nd) v[r] = -FLT_MAX;
+          }
+          *reinterpret_cast<float4*>(dst + db * 16 + 4 * (lane >> 4)) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Step 4: one wave per row over its nsel x 64 candidates.
+template <int KM>
+__global__ __launch_bounds__(256) void hn_final_kernel(const float* __restrict__ cand, const int32_t* __restrict__ sel,
+                                                       long bq, long nch, int k, int32_t* __restrict__ idx,
+                                                       float* __restrict__ val) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= bq) return;
+  const int nsel = (int)(nch < k ? nch : k);
+  float lv[KM];
+  int li[KM];
+  ttk::init<KM>(lv, li);
+  for (int s = 0; s < nsel; ++s) {
+    const int col = sel[row * k + s] * SC_COLS + lane;
+    ttk::insert<KM>(lv, li, k, cand[(row * k + s) * SC_COLS + lane], col);
+  }
+  float ov[KM];
+  int oi[KM];
+  ttk::wave_topk<KM>(lv, li, k, ov, oi);
+  if (lane == 0) {
+    for (int q = 0; q < k; ++q) {
+      idx[row * k + q] = oi[q];
+      if (val) val[row * k + q] = ov[q];
+    }
+  }
+}
+
+struct HnPlan {
+  long nch, RT, S, tps;
+  long off_sel, off_cand, bytes;
+};
+
+long al256(long x) { return (x + 255) & ~255L; }
+
+HnPlan hn_plan(long bq, long nd, int k) {
+  HnPlan p{};
+  p.nch = (nd + SC_COLS - 1) / SC_COLS;
+  p.RT = (bq + SC_ROWS - 1) / SC_ROWS;
+  long S = (256 + p.RT - 1) / p.RT;
+  const long smin = (p.nch + SC_TPS_MAX - 1) / SC_TPS_MAX;
+  if (S < smin) S = smin;
+  if (S > p.nch) S = p.nch;
+  p.tps = (p.nch + S - 1) / S;
+  p.S = (p.nch + p.tps - 1) / p.tps;
+  p.off_sel = al256(bq * p.nch * 4);
+  p.off_cand = p.off_sel + al256(bq * k * 4);
+  p.bytes = p.off_cand + al256(bq * k * SC_COLS * 4);
+  return p;
+}
+
+template <int KS>
+int hn_run(const bf16_t* qn, long bq, const bf16_t* dn, long nd, long label_offset, int k, int32_t* idx, float* val,
+           char* ws, hipStream_t st) {
+  const HnPlan p = hn_plan(bq, nd, k);
+  float* CM = reinterpret_cast<float*>(ws);
+  int32_t* sel = reinterpret_cast<int32_t*>(ws + p.off_sel);
+  float* cand = reinterpret_cast<float*>(ws + p.off_cand);
+  const int nsel = (int)(p.nch < k ? p.nch : k);
+  hipLaunchKernelGGL((hn_scan_kernel<KS>), dim3((unsigned)(p.RT * p.S)), dim3(SC_WAVES * 64), 0, st, qn, bq, dn, nd, label_offset, (int)p.S,
+                     (int)p.tps, p.nch, CM);
+  TT_CHECK_LAUNCH("hn_scan_kernel");
+  const dim3 rows4((unsigned)tt_ceil_div(bq, 4));
+  if (k <= 8)
+    hipLaunchKernelGGL((hn_select_kernel<8>), rows4, dim3(256), 0, st, CM, bq, p.nch, k, sel);
+  else
+    hipLaunchKernelGGL((hn_select_kernel<16>), rows4, dim3(256), 0, st, CM, bq, p.nch, k, sel);
+  TT_CHECK_LAUNCH("hn_select_kernel");
+  hipLaunchKernelGGL((hn_rescore_kernel<KS>), dim3((unsigned)p.nch), dim3(RS_THREADS), 0, st, qn, bq, dn, nd, label_offset,
+                     k, nsel, sel, cand);
+  TT_CHECK_LAUNCH("hn_rescore_kernel");
+  if (k <= 8)
+    hipLaunchKernelGGL((hn_final_kernel<8>), rows4, dim3(256), 0, st, cand, sel, bq, p.nch, k, idx, val);
+  else
+    hipLaunchKernelGGL((hn_final_kernel<16>), rows4, dim3(256), 0, st, cand, sel, bq, p.nch, k, idx, val);
+  TT_CHECK_LAUNCH("hn_final_kernel");
+  return 0;
+}
+
+}  // namespace
+
+// Used by tt_hardneg_topk (tt_loss.hip) for bf16 operands with h in {128, 256}.
+long tt_hn_scan_ws_size(long bq, long nd, int k) { return hn_plan(bq, nd, k).bytes; }
+
+// TT_HN_GEMM=1 forces the GEMM + split top-k path (tests compare the two bit-exactly: both
+// produce every score with the same MFMA instruction and k order).
+bool tt_hn_scan_supported(int dtype, int h) {
+  const char* env = getenv("TT_HN_GEMM");
+  const bool force_gemm = env != nullptr && env[0] == '1';
+  return !force_gemm && dtype == TT_BF16 && (h == 128 || h == 256);
+}
+
+int tt_hn_scan_topk(const void* qn, long bq, const void* dn, long nd, int h, long label_offset, int k, int32_t* idx,
+                    float* val, void* ws, void* stream) {
+  const bf16_t* q = static_cast<const bf16_t*>(qn);
+  const bf16_t* d = static_cast<const bf16_t*>(dn);
+  char* w = static_cast<char*>(ws);
+  hipStream_t st = (hipStream_t)stream;
+  if (h == 256) return hn_run<8>(q, bq, d, nd, label_offset, k, idx, val, w, st);
+  return hn_run<4>(q, bq, d, nd, label_offset, k, idx, val, w, st);
+}

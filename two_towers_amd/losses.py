@@ -179,7 +179,7 @@ def mine_hard_negatives(query_vecs: torch.Tensor, doc_vecs: torch.Tensor, label_
         idx = torch.empty(B, k, dtype=torch.int32, device=qn.device)
         val = torch.empty(B, k, dtype=torch.float32, device=qn.device) if return_values else None
         lib = _lib.load()
-        ws = torch.empty(lib.tt_hardneg_ws_size(dtype_code(compute_dtype), B, nd), dtype=torch.uint8,
+        ws = torch.empty(lib.tt_hardneg_ws_size(dtype_code(compute_dtype), B, nd, h, k), dtype=torch.uint8,
                          device=qn.device)
         esz = 2 if compute_dtype == torch.bfloat16 else 4
         with timing.region("hardneg_topk", 1, 2.0 * B * nd * h, float(esz * (B + nd) * h + B * k * 4)):

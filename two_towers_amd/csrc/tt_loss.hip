@@ -258,6 +258,108 @@ __global__ __launch_bounds__(256) void margin_bwd_kernel(const float* __restrict
   }
 }
 
+// Batched form for k < MB_ENT / MB_ROWS: one workgroup per 64 rows. Mined negatives
+// repeat across rows (rows of one batch share their hardest documents), so per-element
+// atomics straight from every row pile up on a few ddn rows. Here each workgroup first
+// lists its (document, coefficient, row) entries in LDS, sorts them by document
+// (bitonic, 2048 keys), and adds one coefficient-weighted sum of its q rows per distinct
+// document: at most one atomic per (workgroup, document, element).
+constexpr int MB_ROWS = 64, MB_ENT = 2048;
+
+__global__ __launch_bounds__(256) void margin_bwd_grouped_kernel(const float* __restrict__ qn, long bq,
+                                                                 const float* __restrict__ dn, int h, long label_off,
+                                                                 const int32_t* __restrict__ idx, int k, float margin,
+                                                                 float gscale, float* __restrict__ dqn,
+                                                                 float* __restrict__ ddn) {
+  __shared__ unsigned long long key[MB_ENT];  // document << 32 | entry; inactive = all ones
+  __shared__ float coef[MB_ROWS][2];          // (positive, each negative) per row
+  __shared__ int heads[MB_ENT];
+  __shared__ int nheads;
+  const long r0 = (long)blockIdx.x * MB_ROWS;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int kp = k + 1;  // entry 0 of a row: its positive; 1..k: its negatives
+  for (int e = threadIdx.x; e < MB_ENT; e += 256) key[e] = ~0ull;
+  if (threadIdx.x == 0) nheads = 0;
+  __syncthreads();
+  for (int rl = wave; rl < MB_ROWS; rl += 4) {
+    const long row = r0 + rl;
+    if (row >= bq) break;
+    const float* q = qn + row * h;
+    const long lab = label_off + row;
+    const float* dp = dn + lab * h;
+    float pos = 0.f, neg = 0.f;
+    for (int c = lane; c < h; c += 64) pos += q[c] * dp[c];
+    for (int j = 0; j < k; ++j) {
+      const float* dj = dn + (long)idx[row * k + j] * h;
+      for (int c = lane; c < h; c += 64) neg += q[c] * dj[c];
+    }
+    pos = wave_sum(pos);
+    neg = wave_sum(neg) / k;
+    // torch.clamp(min=0) passes the gradient where the argument is >= 0
+    const bool active = (margin - pos + neg) >= 0.f;
+    const float gn = active ? gscale / k : 0.f;
+    const float gp = active ? -gscale : 0.f;
+    for (int c = lane; c < h; c += 64) {
+      float d = gp * dp[c];
+      for (int j = 0; j < k; ++j) d += gn * dn[(long)idx[row * k + j] * h + c];
+      dqn[row * h + c] = d;
+    }
+    if (active) {
+      if (lane == 0) { coef[rl][0] = gp; coef[rl][1] = gn; }
+      for (int j = lane; j < kp; j += 64) {
+        const long doc = j == 0 ? lab : (long)idx[row * k + j - 1];
+        const int e = rl * kp + j;
+        key[e] = ((unsigned long long)doc << 32) | (unsigned)e;
+      }
+    }
+  }
+  __syncthreads();
+  // bitonic sort, ascending
+  for (int size = 2; size <= MB_ENT; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < MB_ENT / 2; t += 256) {
+        const int i = 2 * t - (t & (stride - 1));
+        const int j = i + stride;
+        const bool up = (i & size) == 0;
+        const unsigned long long a = key[i], b = key[j];
+        if ((a > b) == up) { key[i] = b; key[j] = a; }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < MB_ENT; i += 256) {
+    const unsigned long long v = key[i];
+    if (v != ~0ull && (i == 0 || (key[i - 1] >> 32) != (v >> 32))) heads[atomicAdd(&nheads, 1)] = i;
+  }
+  __syncthreads();
+  const int nh = nheads;
+  for (int u = wave; u < nh; u += 4) {
+    const int i0 = heads[u];
+    const unsigned doc = (unsigned)(key[i0] >> 32);
+    int i1 = i0 + 1;
+    while (i1 < MB_ENT && (unsigned)(key[i1] >> 32) == doc && key[i1] != ~0ull) ++i1;
+    for (int c0 = 0; c0 < h; c0 += 256) {
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int i = i0; i < i1; ++i) {
+        const int e = (int)(key[i] & 0xffffffffu);
+        const int rl = e / kp;
+        const float w = coef[rl][e - rl * kp == 0 ? 0 : 1];
+        const float* q = qn + (r0 + rl) * h;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int c = c0 + lane + 64 * m;
+          if (c < h) acc[m] += w * q[c];
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int c = c0 + lane + 64 * m;
+        if (c < h) atomicAdd(ddn + (long)doc * h + c, acc[m]);
+      }
+    }
+  }
+}
+
 inline int esize(int dtype) { return dtype == TT_DT_BF16 ? 2 : 4; }
 
 struct InfoWs {
@@ -450,6 +552,12 @@ extern "C" int tt_margin_bwd(const float* qn, long bq, const float* dn, long nd,
                              void* stream) {
   TT_CHECK_ARG(label_offset >= 0 && label_offset + bq <= nd && k >= 1, "tt_margin_bwd: bad labels/k");
   if (bq == 0) return 0;
+  if ((long)MB_ROWS * (k + 1) <= MB_ENT && nd < (1L << 31)) {
+    hipLaunchKernelGGL(margin_bwd_grouped_kernel, dim3((unsigned)tt_ceil_div(bq, MB_ROWS)), dim3(256), 0,
+                       (hipStream_t)stream, qn, bq, dn, h, label_offset, idx, k, margin, gscale, dqn, ddn);
+    TT_CHECK_LAUNCH("margin_bwd_grouped_kernel");
+    return 0;
+  }
   hipLaunchKernelGGL(margin_bwd_kernel, dim3((unsigned)tt_ceil_div(bq, 4)), dim3(256), 0, (hipStream_t)stream, qn, bq,
                      dn, h, label_offset, idx, k, margin, gscale, dqn, ddn);
   TT_CHECK_LAUNCH("margin_bwd_kernel");

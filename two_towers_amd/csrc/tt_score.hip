@@ -285,11 +285,12 @@ __global__ __launch_bounds__(256) void hn_select_kernel(const float* __restrict_
     for (int q = 0; q < nsel; ++q) sel[row * k + q] = oi[q];
 }
 
-// Step 3: one workgroup per chunk c. It collects the (row, slot) entries that selected c
-// (a scan of sel; LDS list), then its waves rescore them 16 rows at a time with the
-// MFMA orientation and k order of step 1: the chunk's documents as A (registers), the
-// gathered query rows as B.
-constexpr int RS_LIST = 8192;
+// Step 3: one workgroup per (chunk c, segment of RS_SEG rows). It collects the (row,
+// slot) entries of its segment that selected c (a scan of sel; LDS list), then its waves
+// rescore them 16 rows at a time with the MFMA orientation and k order of step 1: the
+// chunk's documents as A (registers), the gathered query rows as B. The segments bound
+// the work of one workgroup when every row selects the same chunks (correlated rows).
+constexpr int RS_SEG = 1024;
 constexpr int RS_THREADS = 512;
 
 template <int KS>
@@ -298,65 +299,64 @@ __global__ __launch_bounds__(RS_THREADS) void hn_rescore_kernel(const bf16_t* __
                                                          int nsel, const int32_t* __restrict__ sel,
                                                          float* __restrict__ cand) {
   constexpr int h = 32 * KS;
-  __shared__ int list[RS_LIST];
+  __shared__ int list[RS_SEG];  // a row selects a chunk at most once
   __shared__ int lcount;
   const int c = blockIdx.x;
   const long n0 = (long)c * SC_COLS;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long seg = (long)blockIdx.y * RS_SEG;
+  const long seg1 = seg + RS_SEG < bq ? seg + RS_SEG : bq;
+  if (threadIdx.x == 0) lcount = 0;
+  __syncthreads();
+  // the segment's entries, 4 per 16-byte load (seg * k is a multiple of 4)
+  const int total = (int)(seg1 - seg) * k;
+  const int4* s4 = reinterpret_cast<const int4*>(sel + seg * k);
+#pragma unroll 4
+  for (int i = threadIdx.x; i < total / 4; i += RS_THREADS) {
+    const int4 v = s4[i];
+    const int w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (w[j] == c && (nsel == k || (4 * i + j) % k < nsel)) list[atomicAdd(&lcount, 1)] = 4 * i + j;
+  }
+  for (int e = total / 4 * 4 + threadIdx.x; e < total; e += RS_THREADS)
+    if (sel[seg * k + e] == c && (nsel == k || e % k < nsel)) list[atomicAdd(&lcount, 1)] = e;
+  __syncthreads();
+  const int n = lcount;
+  if (wave * 16 >= n) return;
   uint4 fa[4][KS];
 #pragma unroll
   for (int db = 0; db < 4; ++db)
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) fa[db][ks] = ld_frag(D, n0 + db * 16 + (lane & 15), nd, h, ks);
-  for (long seg = 0; seg < bq; seg += RS_LIST) {  // a row selects a chunk at most once
-    const long seg1 = seg + RS_LIST < bq ? seg + RS_LIST : bq;
-    if (threadIdx.x == 0) lcount = 0;
-    __syncthreads();
-    // the segment's entries, 4 per 16-byte load, several loads in flight per thread
-    const int total = (int)(seg1 - seg) * k;
-    const int4* s4 = reinterpret_cast<const int4*>(sel + seg * k);
-#pragma unroll 4
-    for (int i = threadIdx.x; i < total / 4; i += RS_THREADS) {
-      const int4 v = s4[i];
-      const int w[4] = {v.x, v.y, v.z, v.w};
+  for (int g = wave; g * 16 < n; g += RS_THREADS / 64) {
+    const int ei = g * 16 + (lane & 15);
+    const long e = ei < n ? seg * k + list[ei] : -1;
+    const long row = e >= 0 ? e / k : bq;  // bq -> zero fragment
+    f32x4 acc[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (w[j] == c && (nsel == k || (4 * i + j) % k < nsel)) list[atomicAdd(&lcount, 1)] = 4 * i + j;
+    for (int db = 0; db < 4; ++db) acc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const uint4 qf = ld_frag(Q, row, bq, h, ks);
+#pragma unroll
+      for (int db = 0; db < 4; ++db) acc[db] = ttg::mma<bf16_t>(fa[db][ks], qf, acc[db]);
     }
-    for (int e = total / 4 * 4 + threadIdx.x; e < total; e += RS_THREADS)
-      if (sel[seg * k + e] == c && (nsel == k || e % k < nsel)) list[atomicAdd(&lcount, 1)] = e;
-    __syncthreads();
-    const int n = lcount;
-    for (int g = wave; g * 16 < n; g += RS_THREADS / 64) {
-      const int ei = g * 16 + (lane & 15);
-      const long e = ei < n ? seg * k + list[ei] : -1;
-      const long row = e >= 0 ? e / k : bq;  // bq -> zero fragment
-      f32x4 acc[4];
+    if (e >= 0) {
+      float* dst = cand + e * SC_COLS;  // e = row * k + slot
 #pragma unroll
-      for (int db = 0; db < 4; ++db) acc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int db = 0; db < 4; ++db) {
+        float v[4];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const uint4 qf = ld_frag(Q, row, bq, h, ks);
-#pragma unroll
-        for (int db = 0; db < 4; ++db) acc[db] = ttg::mma<bf16_t>(fa[db][ks], qf, acc[db]);
-      }
-      if (e >= 0) {
-        float* dst = cand + e * SC_COLS;  // e = row * k + slot
-#pragma unroll
-        for (int db = 0; db < 4; ++db) {
-          float v[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const long doc = n0 + db * 16 + 4 * (lane >> 4) + r;
-            v[r] = acc[db][r];
-            if (label_off >= 0 && doc == label_off + row) v[r] = -1.f;
-            if (doc >= nd) v[r] = -FLT_MAX;
-          }
-          *reinterpret_cast<float4*>(dst + db * 16 + 4 * (lane >> 4)) = make_float4(v[0], v[1], v[2], v[3]);
+        for (int r = 0; r < 4; ++r) {
+          const long doc = n0 + db * 16 + 4 * (lane >> 4) + r;
+          v[r] = acc[db][r];
+          if (label_off >= 0 && doc == label_off + row) v[r] = -1.f;
+          if (doc >= nd) v[r] = -FLT_MAX;
         }
+        *reinterpret_cast<float4*>(dst + db * 16 + 4 * (lane >> 4)) = make_float4(v[0], v[1], v[2], v[3]);
       }
     }
-    __syncthreads();
   }
 }
 
@@ -427,7 +427,7 @@ int hn_run(const bf16_t* qn, long bq, const bf16_t* dn, long nd, long label_offs
   else
     hipLaunchKernelGGL((hn_select_kernel<16>), rows4, dim3(256), 0, st, CM, bq, p.nch, k, sel);
   TT_CHECK_LAUNCH("hn_select_kernel");
-  hipLaunchKernelGGL((hn_rescore_kernel<KS>), dim3((unsigned)p.nch), dim3(RS_THREADS), 0, st, qn, bq, dn, nd, label_offset,
+  hipLaunchKernelGGL((hn_rescore_kernel<KS>), dim3((unsigned)p.nch, (unsigned)tt_ceil_div(bq, RS_SEG)), dim3(RS_THREADS), 0, st, qn, bq, dn, nd, label_offset,
                      k, nsel, sel, cand);
   TT_CHECK_LAUNCH("hn_rescore_kernel");
   if (k <= 8)

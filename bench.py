@@ -65,6 +65,21 @@ def make_batches(n, B, T, V, gen, device):
     return out
 
 
+def workload_name(args, world):
+    """The BASELINE.json config the flags describe (configs[2] by default)."""
+    std = (args.emb, args.hidden, args.seq, args.batch) == (300, 256, 64, 8192) and args.dtype == "bf16"
+    tag = ""
+    if std and args.loss == "hardneg_margin":
+        tag = "BASELINE configs[3]: " if world == 8 else "BASELINE configs[2]: "
+    elif (args.emb, args.hidden, args.seq, args.batch, args.dtype, args.loss) == (300, 256, 64, 1024, "fp32", "infonce"):
+        tag = "BASELINE configs[1]: "
+    elif (args.emb, args.hidden, args.seq, args.dtype) == (300, 512, 128, "bf16"):
+        tag = "BASELINE configs[4] (per-GPU share): "
+    loss = ("hard-negative mining k=5 + margin 0.2" if args.loss == "hardneg_margin" else "in-batch InfoNCE (tau 0.07)")
+    return (f"{tag}EnhancedTwoTowerModel({args.emb}, {args.hidden}), seq_len {args.seq}, batch {args.batch} per GPU, "
+            f"{args.dtype}, {loss}, dropout 0.1, Adam")
+
+
 def cpu_baseline(args):
     """The CPU oracle (PyTorch-CPU restatement of the reference, fp32) on a bounded
     sample of the same workload: same model size, seq_len, loss; smaller batch."""
@@ -250,10 +265,7 @@ def main():
             "vs_baseline": None, "dtype": args.dtype,
             "data": f"synthetic: uniform token ids over a {V}x{E} Word2Vec-shaped table resident in HBM, "
                     f"10% pad tail per row, random-init weights (torch seed 1234)",
-            "config": {"workload": ("BASELINE configs[2]: EnhancedTwoTowerModel(300, 256), seq_len 64, "
-                                    "batch 8192 per GPU, hard-negative mining k=5 + margin 0.2, dropout 0.1, Adam"
-                                    if args.loss == "hardneg_margin" else
-                                    "EnhancedTwoTowerModel(300, 256), seq_len 64, batch 8192 per GPU, InfoNCE"),
+            "config": {"workload": workload_name(args, world),
                        "global_batch": B * world, "seq_len": T, "hidden": h, "embedding_dim": E,
                        "parallelism": f"dp{world}", "loss": args.loss},
             "roofline": roofline,

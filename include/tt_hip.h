@@ -261,10 +261,13 @@ long tt_search_ws_size(int dtype, long Q, long N, int h, int k);
 int tt_margin_fwd(const float* qn, long bq, const float* dn, long nd, int h, long label_offset,
                   const int32_t* idx, int k, float margin, float* row_loss, void* stream);
 /* Gradient of gscale * sum_i row_loss_i: dqn (overwritten), ddn (accumulated; the
- * caller zeroes it). */
+ * caller zeroes it). ws: tt_margin_bwd_ws_size bytes (8 per row) or NULL; with it and
+ * h <= 512, 64 (k + 1) <= 2048, repeated negatives are summed per 64-row group before
+ * the atomics into ddn (hard negatives are shared by many rows). */
 int tt_margin_bwd(const float* qn, long bq, const float* dn, long nd, int h, long label_offset,
                   const int32_t* idx, int k, float margin, float gscale, float* dqn, float* ddn,
-                  void* stream);
+                  void* ws, void* stream);
+long tt_margin_bwd_ws_size(long bq);
 
 /* out[0] = scale * sum_i x[i]. */
 int tt_sum(const float* x, long n, float scale, float* out, void* stream);

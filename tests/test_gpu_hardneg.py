@@ -169,9 +169,11 @@ def test_margin_bwd_repeated_negatives(B, nd, h, k, lab, hot):
     rq, rd = ref_margin_grads(q, d, lab, idx, margin, gscale)
     qd, dd, idd = q.to(DEV), d.to(DEV), idx.to(DEV)
     dq = torch.empty(B, h, device=DEV)
-    ddn = torch.zeros(nd, h, device=DEV)
-    call("tt_margin_bwd", qd.data_ptr(), B, dd.data_ptr(), nd, h, lab, idd.data_ptr(), k, margin, gscale,
-         dq.data_ptr(), ddn.data_ptr(), torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
-    assert (dq.cpu().double() - rq).abs().max() < 1e-6
-    assert (ddn.cpu().double() - rd).abs().max() < 1e-5 * float(rd.abs().max()) + 1e-7
+    for use_ws in (True, False):  # grouped kernels / per-row atomic kernel
+        ddn = torch.zeros(nd, h, device=DEV)
+        ws = torch.empty(_lib.load().tt_margin_bwd_ws_size(B), dtype=torch.uint8, device=DEV)
+        call("tt_margin_bwd", qd.data_ptr(), B, dd.data_ptr(), nd, h, lab, idd.data_ptr(), k, margin, gscale,
+             dq.data_ptr(), ddn.data_ptr(), ws.data_ptr() if use_ws else None, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert (dq.cpu().double() - rq).abs().max() < 1e-6
+        assert (ddn.cpu().double() - rd).abs().max() < 1e-5 * float(rd.abs().max()) + 1e-7

@@ -258,64 +258,75 @@ __global__ __launch_bounds__(256) void margin_bwd_kernel(const float* __restrict
   }
 }
 
-// Batched form for k < MB_ENT / MB_ROWS: one workgroup per 64 rows. Mined negatives
-// repeat across rows (rows of one batch share their hardest documents), so per-element
-// atomics straight from every row pile up on a few ddn rows. Here each workgroup first
-// lists its (document, coefficient, row) entries in LDS, sorts them by document
-// (bitonic, 2048 keys), and adds one coefficient-weighted sum of its q rows per distinct
-// document: at most one atomic per (workgroup, document, element).
-constexpr int MB_ROWS = 64, MB_ENT = 2048;
+// Batched form (h <= 512, 64 * (k + 1) <= 2048): mined negatives repeat across rows
+// (rows of one batch share their hardest documents), so per-element atomics straight
+// from every row pile up on a few ddn rows. Two launches instead:
+//   margin_rows_kernel : one wave per row (all rows in flight): dqn and the row's
+//                        coefficients (positive -gscale, each negative gscale / k; 0 when
+//                        the hinge is inactive);
+//   margin_ddn_kernel  : one workgroup per 64 rows: its q rows staged in LDS, its
+//                        (document, entry) keys sorted by document (bitonic, 2048 keys),
+//                        then one coefficient-weighted sum of q rows per distinct
+//                        document and one atomic per (workgroup, document, element).
+constexpr int MB_ROWS = 64, MB_ENT = 2048, MB_HMAX = 512;
 
-__global__ __launch_bounds__(256) void margin_bwd_grouped_kernel(const float* __restrict__ qn, long bq,
-                                                                 const float* __restrict__ dn, int h, long label_off,
-                                                                 const int32_t* __restrict__ idx, int k, float margin,
-                                                                 float gscale, float* __restrict__ dqn,
-                                                                 float* __restrict__ ddn) {
-  __shared__ unsigned long long key[MB_ENT];  // document << 32 | entry; inactive = all ones
-  __shared__ float coef[MB_ROWS][2];          // (positive, each negative) per row
+__global__ __launch_bounds__(256) void margin_rows_kernel(const float* __restrict__ qn, long bq,
+                                                          const float* __restrict__ dn, int h, long label_off,
+                                                          const int32_t* __restrict__ idx, int k, float margin,
+                                                          float gscale, float* __restrict__ dqn,
+                                                          float2* __restrict__ coef) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= bq) return;
+  const float* q = qn + row * h;
+  const float* dp = dn + (label_off + row) * h;
+  float pos = 0.f, neg = 0.f;
+  for (int c = lane; c < h; c += 64) pos += q[c] * dp[c];
+  for (int j = 0; j < k; ++j) {
+    const float* dj = dn + (long)idx[row * k + j] * h;
+    for (int c = lane; c < h; c += 64) neg += q[c] * dj[c];
+  }
+  pos = wave_sum(pos);
+  neg = wave_sum(neg) / k;
+  // torch.clamp(min=0) passes the gradient where the argument is >= 0
+  const bool active = (margin - pos + neg) >= 0.f;
+  const float gn = active ? gscale / k : 0.f;
+  const float gp = active ? -gscale : 0.f;
+  for (int c = lane; c < h; c += 64) {
+    float d = gp * dp[c];
+    for (int j = 0; j < k; ++j) d += gn * dn[(long)idx[row * k + j] * h + c];
+    dqn[row * h + c] = d;
+  }
+  if (lane == 0) coef[row] = make_float2(gp, gn);
+}
+
+__global__ __launch_bounds__(256) void margin_ddn_kernel(const float* __restrict__ qn, long bq, int h, long label_off,
+                                                         const int32_t* __restrict__ idx, int k,
+                                                         const float2* __restrict__ coef,
+                                                         float* __restrict__ ddn) {
+  __shared__ unsigned long long key[MB_ENT];  // document << 32 | entry; unused = all ones
+  __shared__ float2 cf[MB_ROWS];
   __shared__ int heads[MB_ENT];
   __shared__ int nheads;
+  __shared__ __attribute__((aligned(16))) float qs[MB_ROWS * MB_HMAX];
   const long r0 = (long)blockIdx.x * MB_ROWS;
+  const int nr = (int)(bq - r0 < MB_ROWS ? bq - r0 : MB_ROWS);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int kp = k + 1;  // entry 0 of a row: its positive; 1..k: its negatives
   for (int e = threadIdx.x; e < MB_ENT; e += 256) key[e] = ~0ull;
+  for (int e = threadIdx.x; e < nr * h; e += 256) qs[e] = qn[r0 * h + e];
+  if (threadIdx.x < MB_ROWS) cf[threadIdx.x] = threadIdx.x < nr ? coef[r0 + threadIdx.x] : make_float2(0.f, 0.f);
   if (threadIdx.x == 0) nheads = 0;
   __syncthreads();
-  for (int rl = wave; rl < MB_ROWS; rl += 4) {
-    const long row = r0 + rl;
-    if (row >= bq) break;
-    const float* q = qn + row * h;
-    const long lab = label_off + row;
-    const float* dp = dn + lab * h;
-    float pos = 0.f, neg = 0.f;
-    for (int c = lane; c < h; c += 64) pos += q[c] * dp[c];
-    for (int j = 0; j < k; ++j) {
-      const float* dj = dn + (long)idx[row * k + j] * h;
-      for (int c = lane; c < h; c += 64) neg += q[c] * dj[c];
-    }
-    pos = wave_sum(pos);
-    neg = wave_sum(neg) / k;
-    // torch.clamp(min=0) passes the gradient where the argument is >= 0
-    const bool active = (margin - pos + neg) >= 0.f;
-    const float gn = active ? gscale / k : 0.f;
-    const float gp = active ? -gscale : 0.f;
-    for (int c = lane; c < h; c += 64) {
-      float d = gp * dp[c];
-      for (int j = 0; j < k; ++j) d += gn * dn[(long)idx[row * k + j] * h + c];
-      dqn[row * h + c] = d;
-    }
-    if (active) {
-      if (lane == 0) { coef[rl][0] = gp; coef[rl][1] = gn; }
-      for (int j = lane; j < kp; j += 64) {
-        const long doc = j == 0 ? lab : (long)idx[row * k + j - 1];
-        const int e = rl * kp + j;
-        key[e] = ((unsigned long long)doc << 32) | (unsigned)e;
-      }
+  for (int e = threadIdx.x; e < nr * kp; e += 256) {
+    const int rl = e / kp, j = e - rl * kp;
+    if (cf[rl].x != 0.f) {
+      const long doc = j == 0 ? label_off + r0 + rl : (long)idx[(r0 + rl) * k + j - 1];
+      key[e] = ((unsigned long long)doc << 32) | (unsigned)e;
     }
   }
   __syncthreads();
-  // bitonic sort, ascending
-  for (int size = 2; size <= MB_ENT; size <<= 1) {
+  for (int size = 2; size <= MB_ENT; size <<= 1) {  // bitonic sort, ascending
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       for (int t = threadIdx.x; t < MB_ENT / 2; t += 256) {
         const int i = 2 * t - (t & (stride - 1));
@@ -336,19 +347,16 @@ __global__ __launch_bounds__(256) void margin_bwd_grouped_kernel(const float* __
   for (int u = wave; u < nh; u += 4) {
     const int i0 = heads[u];
     const unsigned doc = (unsigned)(key[i0] >> 32);
-    int i1 = i0 + 1;
-    while (i1 < MB_ENT && (unsigned)(key[i1] >> 32) == doc && key[i1] != ~0ull) ++i1;
     for (int c0 = 0; c0 < h; c0 += 256) {
       float acc[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int i = i0; i < i1; ++i) {
+      for (int i = i0; i < MB_ENT && key[i] != ~0ull && (unsigned)(key[i] >> 32) == doc; ++i) {
         const int e = (int)(key[i] & 0xffffffffu);
         const int rl = e / kp;
-        const float w = coef[rl][e - rl * kp == 0 ? 0 : 1];
-        const float* q = qn + (r0 + rl) * h;
+        const float w = e - rl * kp == 0 ? cf[rl].x : cf[rl].y;
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const int c = c0 + lane + 64 * m;
-          if (c < h) acc[m] += w * q[c];
+          if (c < h) acc[m] += w * qs[rl * h + c];
         }
       }
 #pragma unroll
@@ -547,15 +555,21 @@ extern "C" int tt_margin_fwd(const float* qn, long bq, const float* dn, long nd,
   return 0;
 }
 
+extern "C" long tt_margin_bwd_ws_size(long bq) { return bq > 0 ? bq * 8 : 8; }
+
 extern "C" int tt_margin_bwd(const float* qn, long bq, const float* dn, long nd, int h, long label_offset,
                              const int32_t* idx, int k, float margin, float gscale, float* dqn, float* ddn,
-                             void* stream) {
+                             void* ws, void* stream) {
   TT_CHECK_ARG(label_offset >= 0 && label_offset + bq <= nd && k >= 1, "tt_margin_bwd: bad labels/k");
   if (bq == 0) return 0;
-  if ((long)MB_ROWS * (k + 1) <= MB_ENT && nd < (1L << 31)) {
-    hipLaunchKernelGGL(margin_bwd_grouped_kernel, dim3((unsigned)tt_ceil_div(bq, MB_ROWS)), dim3(256), 0,
-                       (hipStream_t)stream, qn, bq, dn, h, label_offset, idx, k, margin, gscale, dqn, ddn);
-    TT_CHECK_LAUNCH("margin_bwd_grouped_kernel");
+  if ((long)MB_ROWS * (k + 1) <= MB_ENT && h <= MB_HMAX && nd < (1L << 31) && ws) {
+    float2* coef = static_cast<float2*>(ws);
+    hipLaunchKernelGGL(margin_rows_kernel, dim3((unsigned)tt_ceil_div(bq, 4)), dim3(256), 0, (hipStream_t)stream, qn,
+                       bq, dn, h, label_offset, idx, k, margin, gscale, dqn, coef);
+    TT_CHECK_LAUNCH("margin_rows_kernel");
+    hipLaunchKernelGGL(margin_ddn_kernel, dim3((unsigned)tt_ceil_div(bq, MB_ROWS)), dim3(256), 0, (hipStream_t)stream,
+                       qn, bq, h, label_offset, idx, k, coef, ddn);
+    TT_CHECK_LAUNCH("margin_ddn_kernel");
     return 0;
   }
   hipLaunchKernelGGL(margin_bwd_kernel, dim3((unsigned)tt_ceil_div(bq, 4)), dim3(256), 0, (hipStream_t)stream, qn, bq,

@@ -133,8 +133,9 @@ class _MarginFn(torch.autograd.Function):
         B, h = qn.shape
         dqn = torch.empty_like(qn)
         ddn = torch.zeros_like(dn)
+        ws = torch.empty(_lib.load().tt_margin_bwd_ws_size(B), dtype=torch.uint8, device=qn.device)
         call("tt_margin_bwd", qn.data_ptr(), B, dn.data_ptr(), dn.shape[0], h, label_offset, idx.data_ptr(),
-             idx.shape[1], margin, float(gout), dqn.data_ptr(), ddn.data_ptr(), stream_ptr(qn.device))
+             idx.shape[1], margin, float(gout), dqn.data_ptr(), ddn.data_ptr(), ws.data_ptr(), stream_ptr(qn.device))
         return ops.l2norm_bwd(dqn, qn, qnorm, eps), ops.l2norm_bwd(ddn, dn, dnorm, eps), None, None, None, None
 
 

@@ -52,12 +52,15 @@ constexpr int BM = 128, BN = 128;  // tile of the register-staged / small path
 // n-tile) with the n-tile fastest, so the tiles of one A panel, and all tiles of one
 // split-K slice, share an XCD's L2.
 using ttg::xcd_remap;
+#ifndef TT_GEMM_BAL
+#define TT_GEMM_BAL true
+#endif
 
 template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO, int TBM, int TBN, int WGM, int WGN, bool DMA>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_kernel(GemmArgs g) {
   using ML = std::conditional_t<
       DMA,
-      std::conditional_t<TBM == 256 && TBN == 256 && WGM == 2 && WGN == 4, ttg::Loop8<T, AKO, BKO>,
+      std::conditional_t<TBM == 256 && TBN == 256 && WGM == 2 && WGN == 4, ttg::Loop8<T, AKO, BKO, TT_GEMM_BAL>,
                          ttg::DLoop<T, AKO, BKO, TBM, TBN, WGM, WGN>>,
       ttg::MainLoop<T, AKO, BKO, TBM, TBN>>;
   static_assert(DMA || (TBM == 128 && TBN == 128 && WGM == 2 && WGN == 2), "register path is 128x128");

@@ -448,7 +448,7 @@ struct DLoop {
 // 256^2 8-phase template: counted vmcnt, raw s_barrier, all LDS in one array). Every wave
 // issues 2 DMAs per half-tile, always (a K-tile past the slice end reads the zero page),
 // so the counts are exact.
-template <typename T, bool AKO, bool BKO>
+template <typename T, bool AKO, bool BKO, bool BAL = false>
 struct Loop8 {
   static constexpr int HALF = 16384, SLOT = 4 * HALF, LDS_BYTES = 2 * SLOT;
   static constexpr int TM = 8, TN = 4;
@@ -567,6 +567,36 @@ struct Loop8 {
       const uint32_t cur = base + cs * SLOT, nxt = base + (cs ^ 1) * SLOT;
       const char* ia = lds + cs * SLOT + wr * HALF;
       const char* ib = lds + cs * SLOT + (2 + bh) * HALF;
+      if constexpr (BAL) {
+        // balanced reads: P1 A rows 0-63 + B columns 0-31 (12 reads), P2 B columns 32-63
+        // (4), P3 A rows 64-127 (8); B is last read in P2, so both B halves of K-tile
+        // r+2 are restaged in P4 (two phases later)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) fa[ks][i] = frag2<T, AKO>(ia, 16 * i, ks);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) fb[ks][j] = frag2<T, BKO>(ib, bc + 16 * j, ks);
+        }
+        issue_half(la, pa0, r + 1, da, nxt);
+        quad(0, 0, fa, fb, acc);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int j = 2; j < 4; ++j) fb[ks][j] = frag2<T, BKO>(ib, bc + 16 * j, ks);
+        issue_half(la, pa1, r + 1, da, nxt + HALF);
+        quad(0, 1, fa, fb, acc);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) fa[ks][i] = frag2<T, AKO>(ia, 64 + 16 * i, ks);
+        quad(1, 1, fa, fb, acc);
+        issue_half(lb, pb0, r + 2, db, cur + 2 * HALF);
+        issue_half(lb, pb1, r + 2, db, cur + 3 * HALF);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        quad(1, 0, fa, fb, acc);
+        continue;
+      }
       // P1
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {

@@ -326,6 +326,13 @@ __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
   }
 }
 
+TT_DEV void unpack8(uint4 v, float (&f)[8]) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xFFFF0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xFFFF0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xFFFF0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xFFFF0000u);
+}
+
 // ---- backward step on 256x256 tiles (bf16): the recurrent GEMM on the 8-phase loop --
 // One workgroup (8 waves) per 256 rows x 256 hidden units of a recurrence: at B 8192,
 // H 512 the four recurrences are exactly 256 tiles, one per CU, so the GEMM runs at the
@@ -356,7 +363,12 @@ __global__ __launch_bounds__(512) void gru_bwd_big(BwdArgs a) {
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (!last) {
+#ifdef TT_DIAG
+  const int dbg = a.dbg;  // diagnostic build only: 1 no GEMM, 2 no epilogue loads, 4 no stores
+#else
+  constexpr int dbg = 0;
+#endif
+  if (!last && !(dbg & 1)) {
     const bf16_t* DGX = static_cast<const bf16_t*>(R.dgx);
     const bf16_t* DGH = static_cast<const bf16_t*>(R.dgh);
     ttg::KCSplit<bf16_t> la{DGX + (long)tn * a.ldd, DGH + (long)tn * a.ldd, (long)T_ * a.ldd, m0, a.B, 2 * H};
@@ -380,6 +392,13 @@ __global__ __launch_bounds__(512) void gru_bwd_big(BwdArgs a) {
   const int jg = (tid & 31) * 8;
   const int j = j0 + jg;
   const __amdgpu_buffer_rsrc_t grs = tt_rsrc(DGXw + ((long)m0 * T_ + t) * a.ldd);
+  // epilogue operands as buffer resources based at the tile's first row (per-lane byte
+  // offsets < 2 GiB, checked on the host); an absent operand gets num_records 0 and an
+  // out-of-range row offset 0x80000000, so both read zeros without a branch
+  const __amdgpu_buffer_rsrc_t rc = tt_rsrc_n(cr_nxt + (long)m0 * H, !last);
+  const __amdgpu_buffer_rsrc_t rd = tt_rsrc_n(DY ? DY + ((long)m0 * T_ + t) * a.ldy : S, DY != nullptr);
+  const __amdgpu_buffer_rsrc_t rsv = tt_rsrc_n(S + ((long)m0 * T_ + t) * S4, true);
+  const __amdgpu_buffer_rsrc_t ry = tt_rsrc_n(s > 0 ? Y + ((long)m0 * T_ + tp) * a.ldy : S, s > 0);
   float bsum[4][8];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
@@ -395,34 +414,44 @@ __global__ __launch_bounds__(512) void gru_bwd_big(BwdArgs a) {
         for (int r = 0; r < 4; ++r)
           L[((wave >> 2) * 64 + 16 * i + 4 * (lane >> 4) + r) * 256 + wn + 16 * jt + (lane & 15)] = acc[4 * p + i][jt][r];
     __syncthreads();
-#pragma unroll 2
-    for (int k = 0; k < 8; ++k) {
-      const int rl = (tid >> 5) + 16 * k;  // image row: wave row (rl >> 6), row in pass (rl & 63)
-      const int b = m0 + (rl >> 6) * 128 + p * 64 + (rl & 63);
-      if (b < a.B && j < H) {
+    // Rows in batches of NB: the 7 operand loads of every row of a batch are issued back
+    // to back (branch-free: an absent operand reads the zero page), one wait, then the
+    // gate math and the stores. With loads and stores both pending hipcc waits vmcnt(0)
+    // at the next use of a load (MI355X_MICROARCH.md: one in-order counter), so a per-row
+    // load/compute/store loop paid the load and the store latency once per row.
+    constexpr int NB = 2;
+#pragma unroll
+    for (int kb = 0; kb < 8; kb += NB) {
+      uint4 vin[NB][7];
+#pragma unroll
+      for (int kk = 0; kk < NB; ++kk) {
+        // tile row of image row (tid >> 5) + 16 k: wave row k >> 2, row in pass
+        const int bl = (tid >> 5) + p * 64 + 16 * ((kb + kk) & 3) + 128 * ((kb + kk) >> 2);
+        const bool ok = m0 + bl < a.B && !(dbg & 2);
+        const uint32_t oc = ok ? (uint32_t)(bl * H + j) * 2u : 0x80000000u;
+        const uint32_t oy = ok ? (uint32_t)(bl * T_ * (int)a.ldy + j) * 2u : 0x80000000u;
+        const uint32_t os = ok ? (uint32_t)(bl * T_ * (int)S4 + j) * 2u : 0x80000000u;
+        vin[kk][0] = ld16_buf(rc, oc, 0);
+        vin[kk][1] = ld16_buf(rd, oy, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) vin[kk][2 + q] = ld16_buf(rsv, os, q * 2 * H);
+        vin[kk][6] = ld16_buf(ry, oy, 0);
+      }
+#pragma unroll
+      for (int kk = 0; kk < NB; ++kk) {
+        const int rl = (tid >> 5) + 16 * (kb + kk);
+        const int b = m0 + (rl >> 6) * 128 + p * 64 + (rl & 63);
+        if (b >= a.B) continue;
         const long row = (long)b * T_ + t;
         float cin[8], dy[8], ar[8], az[8], an[8], gh[8], hp[8];
-        if (!last) ld8(cr_nxt + (long)b * H + j, cin);
-        else if (R.dfinal) ld8(R.dfinal + (long)b * a.ldf + j, cin);
-        else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) cin[e] = 0.f;
-        }
-        if (DY) ld8(DY + row * a.ldy + j, dy);
-        else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) dy[e] = 0.f;
-        }
-        const bf16_t* sp = S + row * S4 + j;
-        ld8(sp, ar);
-        ld8(sp + H, az);
-        ld8(sp + 2 * H, an);
-        ld8(sp + 3 * H, gh);
-        if (s > 0) ld8(Y + ((long)b * T_ + tp) * a.ldy + j, hp);
-        else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) hp[e] = 0.f;
-        }
+        unpack8(vin[kk][0], cin);
+        unpack8(vin[kk][1], dy);
+        unpack8(vin[kk][2], ar);
+        unpack8(vin[kk][3], az);
+        unpack8(vin[kk][4], an);
+        unpack8(vin[kk][5], gh);
+        unpack8(vin[kk][6], hp);
+        if (last && R.dfinal) ld8(R.dfinal + (long)b * a.ldf + j, cin);  // fp32 final-state gradient
         const float* Lc = L + rl * 256 + jg;
         float o_r[8], o_z[8], o_n[8], o_hn[8], cout[8];
 #pragma unroll
@@ -438,6 +467,10 @@ __global__ __launch_bounds__(512) void gru_bwd_big(BwdArgs a) {
           o_r[e] = drp; o_z[e] = dzp; o_n[e] = dnp; o_hn[e] = dnp * rg;
           cout[e] = dht * zg;
           bsum[0][e] += drp; bsum[1][e] += dzp; bsum[2][e] += dnp; bsum[3][e] += dnp * rg;
+        }
+        if (dbg & 4) {
+          if (o_r[0] == 12345.f) L[0] = o_z[1] + o_n[2] + o_hn[3] + cout[4];
+          continue;
         }
         st8(cr_cur + (long)b * H + j, cout);
         bf16_t* xw = DGXw + row * a.ldd + j;
@@ -496,12 +529,6 @@ static_assert(P_LDS <= 163840, "persistent GRU LDS budget");
 
 // fp32 gate tile [64 rows][48 chunks of 4]: chunk c of row r at c ^ (r & 15)
 // (conflict-free for the MFMA-layout writes and the 8-float row reads below).
-TT_DEV void unpack8(uint4 v, float (&f)[8]) {
-  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xFFFF0000u);
-  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xFFFF0000u);
-  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xFFFF0000u);
-  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xFFFF0000u);
-}
 
 TT_DEV int stg_off(int row, int col) { return row * 192 + ((((col >> 2) ^ (row & 15))) << 2) + (col & 3); }
 
@@ -614,6 +641,10 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
 #pragma unroll
           for (int g = 0; g < 3; ++g) gx[g] = make_uint4(0, 0, 0, 0);
         }
+        // b_hn with them: a load issued after the K loop would make its wait drain the
+        // W_hh ring prefetches too (one in-order vmcnt)
+        const float4 bn0 = *reinterpret_cast<const float4*>(R.bhn + blk * 64 + jg);
+        const float4 bn1 = *reinterpret_cast<const float4*>(R.bhn + blk * 64 + jg + 4);
         f32x4 acc[2][3];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -643,7 +674,8 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
         unpack8(gx[0], xr);
         unpack8(gx[1], xz);
         unpack8(gx[2], xn);
-        ld8(R.bhn + j, bn);
+        bn[0] = bn0.x; bn[1] = bn0.y; bn[2] = bn0.z; bn[3] = bn0.w;
+        bn[4] = bn1.x; bn[5] = bn1.y; bn[6] = bn1.z; bn[7] = bn1.w;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const float4 v0 = *reinterpret_cast<const float4*>(stg + stg_off(rl, 0 * 64 + jg + 4 * h));

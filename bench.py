@@ -157,11 +157,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # TT_DIST_BACKEND=gloo (rehearsal only): N ranks sharing the box's GPUs over gloo
+    backend = os.environ.get("TT_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     group = None
     if world > 1:
-        tdist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=dev)
+        else:
+            tdist.init_process_group(backend)
     import two_towers_amd as tta
     from two_towers_amd import dist as tdp
     from two_towers_amd import timing

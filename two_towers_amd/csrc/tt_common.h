@@ -69,13 +69,29 @@ typedef unsigned tt_u32x4 __attribute__((vector_size(16)));
 TT_DEV __amdgpu_buffer_rsrc_t tt_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
 }
+TT_DEV uint4 pack8bf(const float (&f)[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+// 16-byte buffer store (default cache policy); an offset past num_records is dropped.
+TT_DEV void st16_buf(__amdgpu_buffer_rsrc_t r, uint32_t voff, int soff, uint4 v) {
+  tt_u32x4 w = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, (int)voff, soff, 0);
+}
+TT_DEV void st16_buf_sc1(__amdgpu_buffer_rsrc_t r, uint32_t voff, int soff, uint4 v) {
+  tt_u32x4 w = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, (int)voff, soff, 16);
+}
 // Buffer resource of num_records 0x7fffffff bytes, or 0 (every load reads zero) if !on.
 TT_DEV __amdgpu_buffer_rsrc_t tt_rsrc_n(const void* base, bool on) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, on ? 0x7fffffff : 0, 0x00020000);
 }
 // 16-byte buffer load; an offset past num_records returns zeros.
+template <int AUX = 0>
 TT_DEV uint4 ld16_buf(__amdgpu_buffer_rsrc_t r, uint32_t voff, int soff) {
-  const tt_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, soff, 0);
+  const tt_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, soff, AUX);
   return make_uint4(v[0], v[1], v[2], v[3]);
 }
 TT_DEV void st16_sc1(__amdgpu_buffer_rsrc_t r, int off, uint4 v) {

@@ -583,7 +583,12 @@ TT_DEV void fwd_kstep(const bf16_t* W, int H, int Q, int q, int kt, bool mm, con
   ++it;
 }
 
-template <int D>  // Whh K-tiles in flight in registers: 1, 2 or 4 (D divides H/64)
+// Whh K-tiles in flight in registers: 1, 2 or 4 (D divides H/64); NKT = H/64 when known
+// at compile time (0: runtime). A compile-time NKT unrolls the block's K loop, so hipcc's
+// vmcnt bookkeeping at its first K-tiles counts the previous block's epilogue stores and
+// the gate loads exactly instead of the loop-merged minimum: with one in-order counter
+// that minimum made the first W_hh waits of every block also wait for those stores.
+template <int D, int NKT>
 __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[P_LDS];
   char* hb = lds;
@@ -595,7 +600,7 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
   const FwdRec R = a.r[rz];
   const int H = a.H, T_ = a.T;
   const int m0 = (id - rz * ntm) * PR;
-  const int nblk = H / 64, nkt = H / 64, Q = nblk * nkt;
+  const int nblk = NKT ? NKT : H / 64, nkt = NKT ? NKT : H / 64, Q = nblk * nkt;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = (wave >> 2) * 32, wn = (wave & 3) * 48;
   const bf16_t* W = static_cast<const bf16_t*>(R.whh);
@@ -607,6 +612,16 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
   const int rl = tid >> 3, jg = (tid & 7) * 8;
   const int b = m0 + rl;
   const bool rowok = b < a.B;
+  // gate inputs and outputs through buffer resources based at this workgroup's first
+  // row: no branches around the memory instructions (a tail row's offset is out of
+  // range, so it reads zeros and its stores are dropped; no X1 = num_records 0), so
+  // every wave issues the same count and the waits above stay exact
+  const long r0w = (long)m0 * T_;
+  const __amdgpu_buffer_rsrc_t rG = tt_rsrc_n(G + r0w * a.ldg, true);
+  const __amdgpu_buffer_rsrc_t rY = tt_rsrc_n(Yw + r0w * a.ldy, true);
+  const __amdgpu_buffer_rsrc_t rX1 = tt_rsrc_n(X1 ? X1 + r0w * a.ldy : Yw, X1 != nullptr);
+  const __amdgpu_buffer_rsrc_t rS = tt_rsrc_n(S + r0w * 4L * H, true);
+  const bool gok = rowok && !(a.dbg & 2), sok = rowok && !(a.dbg & 1);
 
   float hreg[PH_MAX / 64][8];
 #pragma unroll
@@ -624,23 +639,24 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
   }
   int it = 0;  // running K-tile counter: Whh stage = it & 1
   __syncthreads();
+  // six dropped stores (out-of-range offset) stand in for the epilogue's six, so every
+  // path into a block's first K-tiles has the same pending count and hipcc's waits
+  // there leave the stores in flight
+#pragma unroll
+  for (int q = 0; q < 6; ++q) st16_buf(rY, 0x80000000u + 16u * q, 0, make_uint4(0, 0, 0, 0));
 
   for (int s = 0; s < T_; ++s) {
     const int t = R.dir ? T_ - 1 - s : s;
     const long row = (long)b * T_ + t;
-#pragma unroll
+    const int lrow = rl * T_ + t;  // row within this workgroup's resources
+#pragma unroll 1
     for (int blk = 0; blk < nblk; ++blk) {
       {
         // gate inputs of this block's epilogue, issued before the GEMM so they land under it
         uint4 gx[3];
-        if (rowok && !(a.dbg & 2)) {
+        const uint32_t og = gok ? (uint32_t)(lrow * (int)a.ldg + blk * 64 + jg) * 2u : 0x80000000u;
 #pragma unroll
-          for (int g = 0; g < 3; ++g)
-            gx[g] = *reinterpret_cast<const uint4*>(G + row * a.ldg + g * H + blk * 64 + jg);
-        } else {
-#pragma unroll
-          for (int g = 0; g < 3; ++g) gx[g] = make_uint4(0, 0, 0, 0);
-        }
+        for (int g = 0; g < 3; ++g) gx[g] = ld16_buf(rG, og, g * H * 2);
         // b_hn with them: a load issued after the K loop would make its wait drain the
         // W_hh ring prefetches too (one in-order vmcnt)
         const float4 bn0 = *reinterpret_cast<const float4*>(R.bhn + blk * 64 + jg);
@@ -653,10 +669,13 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
         // ring of D register sets: iteration q reads set (q+1)%D, refills set q%D
 #define TT_KS(j, X, Y) fwd_kstep<D>(W, H, Q, blk * nkt + kt + j, kt + j, s > 0, hb, bst, it, wm, wn, acc, X, Y)
         if constexpr (D == 1) {
+#pragma unroll
           for (int kt = 0; kt < nkt; ++kt) TT_KS(0, r0, r0);
         } else if constexpr (D == 2) {
+#pragma unroll
           for (int kt = 0; kt < nkt; kt += 2) { TT_KS(0, r1, r0); TT_KS(1, r0, r1); }
         } else {
+#pragma unroll
           for (int kt = 0; kt < nkt; kt += 4) { TT_KS(0, r1, r0); TT_KS(1, r2, r1); TT_KS(2, r3, r2); TT_KS(3, r0, r3); }
         }
 #undef TT_KS
@@ -698,21 +717,20 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
         float ynew[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) ynew[e] = y[e];
-        if (rowok && !(a.dbg & 1)) {
-          st8(Yw + row * a.ldy + j, y);
-          bf16_t* sp = S + row * (4L * H) + j;
-          st8(sp, sr);
-          st8(sp + H, sz);
-          st8(sp + 2 * H, sn);
-          st8(sp + 3 * H, sg);
-          if (X1) {
+        {
+          const uint32_t oy = sok ? (uint32_t)(lrow * (int)a.ldy + j) * 2u : 0x80000000u;
+          const uint32_t os = sok ? (uint32_t)(lrow * 4 * H + j) * 2u : 0x80000000u;
+          st16_buf(rY, oy, 0, pack8bf(y));
+          st16_buf(rS, os, 0, pack8bf(sr));
+          st16_buf(rS, os, 2 * H, pack8bf(sz));
+          st16_buf(rS, os, 4 * H, pack8bf(sn));
+          st16_buf(rS, os, 6 * H, pack8bf(sg));
+          if (X1 && a.drop_thresh) {
 #pragma unroll
             for (int e = 0; e < 8; ++e)
-              y[e] *= a.drop_thresh ? tt_dropout_scale(R.seed, (uint32_t)row, (uint32_t)(R.col0 + j + e),
-                                                       a.drop_thresh, a.inv_keep)
-                                    : 1.f;
-            st8(X1 + row * a.ldy + j, y);
+              y[e] *= tt_dropout_scale(R.seed, (uint32_t)row, (uint32_t)(R.col0 + j + e), a.drop_thresh, a.inv_keep);
           }
+          st16_buf(rX1, oy, 0, pack8bf(y));
         }
         // stg is rewritten only after the next block's K loop (whose barriers order it)
         // the state of block blk moves to the back: hreg[0] is always the current block
@@ -798,7 +816,7 @@ extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B
   TT_CHECK_ARG(H % 8 == 0 && (ldy * esz) % 16 == 0, "tt_gru_fwd: H=%d (multiple of 8)/ldy=%ld misaligned", H, ldy);
   TT_CHECK_ARG(drop_p >= 0.f && drop_p < 1.f, "tt_gru_fwd: drop_p");
   TT_CHECK_ARG(tt_ceil_div(B, 128) <= 65535, "tt_gru_fwd: B too large");
-  TT_CHECK_ARG(128L * T * std::max(4L * H, ldy) * esz < (1L << 31), "tt_gru_fwd: tile byte offsets exceed 2 GiB");
+  TT_CHECK_ARG(128L * T * std::max({4L * H, ldy, ldg}) * esz < (1L << 31), "tt_gru_fwd: tile byte offsets exceed 2 GiB");
   FwdArgs a{};
   for (int i = 0; i < nrec; ++i) {
     const tt_gru_fwd_rec& r = recs[i];
@@ -814,9 +832,11 @@ extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B
     const dim3 grid(tt_ceil_div(B, PR) * nrec);
     int depth = (H / 64) % 4 == 0 ? 4 : (H / 64) % 2 == 0 ? 2 : 1;
     if (const char* e = getenv("TT_GRU_DEPTH")) depth = std::min(depth, atoi(e));
-    if (depth >= 4) hipLaunchKernelGGL(gru_fwd_seq<4>, grid, dim3(PNT), 0, st, a);
-    else if (depth == 2) hipLaunchKernelGGL(gru_fwd_seq<2>, grid, dim3(PNT), 0, st, a);
-    else hipLaunchKernelGGL(gru_fwd_seq<1>, grid, dim3(PNT), 0, st, a);
+    if (depth >= 4 && H == 512) hipLaunchKernelGGL((gru_fwd_seq<4, 8>), grid, dim3(PNT), 0, st, a);
+    else if (depth >= 4 && H == 256) hipLaunchKernelGGL((gru_fwd_seq<4, 4>), grid, dim3(PNT), 0, st, a);
+    else if (depth >= 4) hipLaunchKernelGGL((gru_fwd_seq<4, 0>), grid, dim3(PNT), 0, st, a);
+    else if (depth == 2) hipLaunchKernelGGL((gru_fwd_seq<2, 0>), grid, dim3(PNT), 0, st, a);
+    else hipLaunchKernelGGL((gru_fwd_seq<1, 0>), grid, dim3(PNT), 0, st, a);
     TT_CHECK_LAUNCH("gru_fwd_seq");
     return 0;
   }
@@ -837,7 +857,7 @@ extern "C" int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B
   TT_CHECK_ARG(B > 0 && T > 0 && H > 0, "tt_gru_bwd: bad shape");
   const int esz = dtype == TT_DT_BF16 ? 2 : 4;
   TT_CHECK_ARG(H % 8 == 0 && (ldd * esz) % 16 == 0, "tt_gru_bwd: H=%d (multiple of 8)/ldd=%ld misaligned", H, ldd);
-  TT_CHECK_ARG(128L * T * ldd * esz < (1L << 31), "tt_gru_bwd: tile byte offsets exceed 2 GiB");
+  TT_CHECK_ARG(256L * T * std::max({ldd, ldy, 4L * H}) * esz < (1L << 31), "tt_gru_bwd: tile byte offsets exceed 2 GiB");
   hipStream_t st = (hipStream_t)stream;
   BwdArgs a{};
   for (int i = 0; i < nrec; ++i) {

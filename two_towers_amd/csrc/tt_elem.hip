@@ -111,7 +111,9 @@ extern "C" int tt_colsum(const float* x, long rows, int cols, long ld, float* ou
   if (!accumulate) TT_CHECK_HIP(hipMemsetAsync(out, 0, sizeof(float) * cols, st));
   if (rows == 0 || cols == 0) return 0;
   const int cb = tt_ceil_div(cols, 256);
-  long slabs = std::max<long>(1, std::min<long>(rows / 64, 2048 / cb));
+  // >= 16 rows per slab, <= 256 workgroups: the GRU bias partials (64 rows x 2048
+  // columns) ran on 8 workgroups of 64 serial loads each (19 us per call)
+  long slabs = std::max<long>(1, std::min<long>(rows / 16, std::max(1, 256 / cb)));
   const long rps = (rows + slabs - 1) / slabs;
   slabs = (rows + rps - 1) / rps;
   hipLaunchKernelGGL(colsum_kernel, dim3(cb, (unsigned)slabs), dim3(256), 0, st, x, rows, cols, ld, rps, out);

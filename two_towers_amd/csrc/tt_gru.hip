@@ -558,9 +558,23 @@ TT_DEV void fwd_store_b(char* img, const WTile& r) {
 // the next step; the very last prefetches are harmless reloads, unconditional so the
 // sets stay in registers), MFMAs on LDS stage it&1, then K-tile q+1 (set X, loaded
 // D-1 tiles ago) into the other stage.
+#ifdef TT_DIAG
+// diagnostic build only: per-phase s_memtime totals of wave 0 of every workgroup
+__device__ unsigned long long g_fwd_prof[2048][8];
+#define TT_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define TT_ACC(i, d) (prf[i] += (d))
+#define TT_PROF_PARAM , unsigned long long (&prf)[8]
+#define TT_PROF_ARGS , prf
+#else
+#define TT_STAMP(v) do { } while (0)
+#define TT_ACC(i, d) do { } while (0)
+#define TT_PROF_PARAM
+#define TT_PROF_ARGS
+#endif
 template <int D>
 TT_DEV void fwd_kstep(const bf16_t* W, int H, int Q, int q, int kt, bool mm, const char* hb, char* bst, int& it,
-                      int wm, int wn, f32x4 (&acc)[2][3], WTile& X, WTile& Y) {
+                      int wm, int wn, f32x4 (&acc)[2][3], WTile& X, WTile& Y TT_PROF_PARAM) {
+  TT_STAMP(t0);
   fwd_load_b(W, H, (q + D) % Q, Y);
   if (mm) {  // h_{-1} = 0: the first step has no recurrent term
     const char* ia = hb + kt * (PR * ttg::KTB);
@@ -578,8 +592,14 @@ TT_DEV void fwd_kstep(const bf16_t* W, int H, int Q, int q, int kt, bool mm, con
         for (int j = 0; j < 3; ++j) acc[i][j] = ttg::mma<bf16_t>(fa[i], fb[j], acc[i][j]);
     }
   }
+  TT_STAMP(t1);
   fwd_store_b(bst + ((it + 1) & 1) * P_BST, X);
+  TT_STAMP(t2);
   __syncthreads();
+  TT_STAMP(t3);
+  TT_ACC(0, t1 - t0);  // W_hh load issue + fragment reads + MFMA
+  TT_ACC(1, t2 - t1);  // wait for the ring set + its LDS store
+  TT_ACC(2, t3 - t2);  // barrier
   ++it;
 }
 
@@ -638,6 +658,10 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
     fwd_load_b(W, H, 3 % Q, r3);
   }
   int it = 0;  // running K-tile counter: Whh stage = it & 1
+#ifdef TT_DIAG
+  unsigned long long prf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  TT_STAMP(k_start);
+#endif
   __syncthreads();
   // six dropped stores (out-of-range offset) stand in for the epilogue's six, so every
   // path into a block's first K-tiles has the same pending count and hipcc's waits
@@ -667,7 +691,7 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
 #pragma unroll
           for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         // ring of D register sets: iteration q reads set (q+1)%D, refills set q%D
-#define TT_KS(j, X, Y) fwd_kstep<D>(W, H, Q, blk * nkt + kt + j, kt + j, s > 0, hb, bst, it, wm, wn, acc, X, Y)
+#define TT_KS(j, X, Y) fwd_kstep<D>(W, H, Q, blk * nkt + kt + j, kt + j, s > 0, hb, bst, it, wm, wn, acc, X, Y TT_PROF_ARGS)
         if constexpr (D == 1) {
 #pragma unroll
           for (int kt = 0; kt < nkt; ++kt) TT_KS(0, r0, r0);
@@ -679,6 +703,7 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
           for (int kt = 0; kt < nkt; kt += 4) { TT_KS(0, r1, r0); TT_KS(1, r2, r1); TT_KS(2, r3, r2); TT_KS(3, r0, r3); }
         }
 #undef TT_KS
+        TT_STAMP(e0);
         // gates -> LDS (fp32), then per-thread rows
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -688,6 +713,8 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
             for (int r = 0; r < 4; ++r)
               stg[stg_off(wm + 16 * i + 4 * (lane >> 4) + r, wn + 16 * j + (lane & 15))] = acc[i][j][r];
         __syncthreads();
+        TT_STAMP(e1);
+        TT_ACC(3, e1 - e0);  // gate staging + barrier
         const int j = blk * 64 + jg;
         float xr[8], xz[8], xn[8], bn[8], lr[8], lz[8], ln[8], y[8], sr[8], sz[8], sn[8], sg[8];
         unpack8(gx[0], xr);
@@ -732,6 +759,8 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
           }
           st16_buf(rX1, oy, 0, pack8bf(y));
         }
+        TT_STAMP(e2);
+        TT_ACC(4, e2 - e1);  // gate math + stores issued
         // stg is rewritten only after the next block's K loop (whose barriers order it)
         // the state of block blk moves to the back: hreg[0] is always the current block
 #pragma unroll
@@ -766,8 +795,21 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
     }
     __syncthreads();
   }
+#ifdef TT_DIAG
+  TT_STAMP(k_end);
+  prf[7] = k_end - k_start;
+  if (threadIdx.x == 0 && blockIdx.x < 2048)
+    for (int i = 0; i < 8; ++i) g_fwd_prof[blockIdx.x][i] = prf[i];
+#endif
 }
 
+#ifdef TT_DIAG
+}  // namespace
+extern "C" int tt_diag_fwd_prof(unsigned long long* out) {  // [2048][8] host buffer
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fwd_prof), sizeof(g_fwd_prof)) == hipSuccess ? 0 : 1;
+}
+namespace {
+#endif
 bool gru_fwd_persistent(int dtype, int H) {
   if (dtype != TT_DT_BF16 || H % 64 != 0 || H > PH_MAX) return false;
   const char* e = getenv("TT_GRU_STEP");

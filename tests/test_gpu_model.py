@@ -149,6 +149,30 @@ def test_cpu_tensors_fail_loudly():
         m(torch.randn(2, 3, 16), torch.randn(2, 3, 16))
 
 
+@pytest.mark.parametrize("h,B,T", [(128, 1100, 4), (256, 2048, 3)])
+def test_persistent_gru_staggered_block_order(h, B, T, monkeypatch):
+    """TT_GRU_STAGGER=1 (H 256 / 512 instances): each workgroup starts its unit-block
+    loop at (blockIdx / 8) mod nblk; same arithmetic per unit, so outputs and gradients
+    agree with the default order to fp32 rounding. B >= 1100 gives every offset."""
+    E = 48
+    g = torch.Generator().manual_seed(12)
+    q = torch.randn(B, T, E, generator=g).to(DEV)
+    d = torch.randn(B, T, E, generator=g).to(DEV)
+    outs = []
+    for stg in ("0", "1"):
+        monkeypatch.setenv("TT_GRU_STAGGER", stg)
+        m, _ = make_model(E, h, 3)
+        m = m.to(DEV).train().set_compute_dtype(torch.bfloat16)
+        qv, dv = m(q, d)
+        loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
+        loss.backward()
+        outs.append((qv.detach().clone(), dv.detach().clone(), {k: p.grad.clone() for k, p in m.named_parameters()}))
+    (q0, d0, g0), (q1, d1, g1) = outs
+    assert rel(q1, q0) < 1e-5 and rel(d1, d0) < 1e-5
+    for k in g0:
+        assert rel(g1[k], g0[k]) < 1e-4, k
+
+
 @pytest.mark.parametrize("h,B,T", [(32, 96, 10), (64, 200, 7), (128, 70, 4), (256, 130, 5)])
 def test_persistent_gru_matches_step_kernel(h, B, T, monkeypatch):
     """bf16 forward + backward through the persistent (row-resident) GRU forward

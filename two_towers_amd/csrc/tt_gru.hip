@@ -29,6 +29,7 @@ struct FwdArgs {
   uint32_t drop_thresh;
   float inv_keep;
   int dbg;  // diagnostics (env TT_GRU_DBG): 1 no stores, 2 no G loads, 4 no MFMA, 8 no Whh stream
+  int stagger;  // persistent forward (compile-time NKT only): env TT_GRU_STAGGER
 };
 
 struct BwdRec {
@@ -642,6 +643,11 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
   const __amdgpu_buffer_rsrc_t rX1 = tt_rsrc_n(X1 ? X1 + r0w * a.ldy : Yw, X1 != nullptr);
   const __amdgpu_buffer_rsrc_t rS = tt_rsrc_n(S + r0w * 4L * H, true);
   const bool gok = rowok && !(a.dbg & 2), sok = rowok && !(a.dbg & 1);
+  // experimental: every step's block order starts at boff so the workgroups of one XCD
+  // (blockIdx.x = x mod 8) stream different W_hh blocks at the same instant; hreg[i]
+  // then holds block (boff + i) mod nblk. Compiled only into the fixed-NKT instances.
+  const int boff = (NKT != 0 && a.stagger) ? (int)((blockIdx.x >> 3) % (unsigned)nblk) : 0;
+  const int qoff = boff * nkt;
 
   float hreg[PH_MAX / 64][8];
 #pragma unroll
@@ -650,12 +656,12 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
     for (int e = 0; e < 8; ++e) hreg[i][e] = 0.f;
 
   WTile r0, r1, r2, r3;
-  fwd_load_b(W, H, 0, r0);
+  fwd_load_b(W, H, qoff, r0);
   fwd_store_b(bst, r0);
-  if (D >= 2) fwd_load_b(W, H, 1 % Q, r1);
+  if (D >= 2) fwd_load_b(W, H, (qoff + 1) % Q, r1);
   if (D >= 4) {
-    fwd_load_b(W, H, 2 % Q, r2);
-    fwd_load_b(W, H, 3 % Q, r3);
+    fwd_load_b(W, H, (qoff + 2) % Q, r2);
+    fwd_load_b(W, H, (qoff + 3) % Q, r3);
   }
   int it = 0;  // running K-tile counter: Whh stage = it & 1
 #ifdef TT_DIAG
@@ -674,7 +680,8 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
     const long row = (long)b * T_ + t;
     const int lrow = rl * T_ + t;  // row within this workgroup's resources
 #pragma unroll 1
-    for (int blk = 0; blk < nblk; ++blk) {
+    for (int blk0 = 0; blk0 < nblk; ++blk0) {
+      const int blk = blk0 + boff < nblk ? blk0 + boff : blk0 + boff - nblk;
       {
         // gate inputs of this block's epilogue, issued before the GEMM so they land under it
         uint4 gx[3];
@@ -783,12 +790,13 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
     // h_s -> A operand of step s+1 (every wave finished reading h_{s-1}: the last
     // K-tile ended with a barrier)
 #pragma unroll
-    for (int blk = 0; blk < PH_MAX / 64; ++blk) {
-      if (blk < nblk) {
+    for (int i = 0; i < PH_MAX / 64; ++i) {
+      if (i < nblk) {
+        const int blk = i + boff < nblk ? i + boff : i + boff - nblk;
         uint32_t w[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          w[i] = (uint32_t)f2bf(hreg[blk][2 * i]) | ((uint32_t)f2bf(hreg[blk][2 * i + 1]) << 16);
+        for (int k = 0; k < 4; ++k)
+          w[k] = (uint32_t)f2bf(hreg[i][2 * k]) | ((uint32_t)f2bf(hreg[i][2 * k + 1]) << 16);
         *reinterpret_cast<uint4*>(hb + blk * (PR * ttg::KTB) + ttg::kc_off(rl, tid & 7)) =
             make_uint4(w[0], w[1], w[2], w[3]);
       }
@@ -869,6 +877,7 @@ extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B
   a.drop_thresh = drop_p > 0.f ? (uint32_t)(drop_p * 16777216.0f + 0.5f) : 0u;
   a.inv_keep = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
   if (const char* e = getenv("TT_GRU_DBG")) a.dbg = atoi(e);
+  if (const char* e = getenv("TT_GRU_STAGGER")) a.stagger = atoi(e);
   hipStream_t st = (hipStream_t)stream;
   if (gru_fwd_persistent(dtype, H)) {
     const dim3 grid(tt_ceil_div(B, PR) * nrec);

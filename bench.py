@@ -13,8 +13,9 @@ i.e. weak scaling at 8192 pairs per rank.
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Rank 0 prints ONE JSON line. `roofline` is measured live with HIP events around the
-dominant kernel's launches; `cpu_baseline` times the CPU oracle (oracle/cpu_ref.py,
-PyTorch-CPU, same model/loss) on a bounded sample on this host's cores.
+dominant kernel's launches; `cpu_baseline` times the reference's own CPU path (ATen
+nn.GRU / nn.Linear / nn.LayerNorm modules, oracle/aten_ref.py) on a bounded sample on
+this host's cores.
 """
 from __future__ import annotations
 
@@ -44,9 +45,13 @@ def parse():
     ap.add_argument("--vocab", type=int, default=3_000_000)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--loss", default="hardneg_margin", choices=["hardneg_margin", "infonce"])
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: --batch pairs per GPU (configs[3]: 8 x 8192); strong: --batch is the global "
+                         "batch, split over the GPUs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=256, help="pairs per CPU-baseline step")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-batch", type=int, default=1024, help="pairs per CPU-baseline step (BASELINE.md plan)")
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-warmup", type=int, default=1)
     ap.add_argument("--timing", action="store_true", help="print the per-kernel HIP-event table to stderr")
     return ap.parse_args()
 
@@ -69,62 +74,69 @@ def workload_name(args, world):
     """The BASELINE.json config the flags describe (configs[2] by default)."""
     std = (args.emb, args.hidden, args.seq, args.batch) == (300, 256, 64, 8192) and args.dtype == "bf16"
     tag = ""
-    if std and args.loss == "hardneg_margin":
+    if std and args.loss == "hardneg_margin" and args.scaling == "strong":
+        tag = f"BASELINE metric (global batch 8192 over {world} GPU): " if world > 1 else "BASELINE configs[2]: "
+    elif std and args.loss == "hardneg_margin":
         tag = "BASELINE configs[3]: " if world == 8 else "BASELINE configs[2]: "
     elif (args.emb, args.hidden, args.seq, args.batch, args.dtype, args.loss) == (300, 256, 64, 1024, "fp32", "infonce"):
         tag = "BASELINE configs[1]: "
     elif (args.emb, args.hidden, args.seq, args.dtype) == (300, 512, 128, "bf16"):
         tag = "BASELINE configs[4] (per-GPU share): "
     loss = ("hard-negative mining k=5 + margin 0.2" if args.loss == "hardneg_margin" else "in-batch InfoNCE (tau 0.07)")
-    return (f"{tag}EnhancedTwoTowerModel({args.emb}, {args.hidden}), seq_len {args.seq}, batch {args.batch} per GPU, "
+    per = args.batch // world if args.scaling == "strong" else args.batch
+    return (f"{tag}EnhancedTwoTowerModel({args.emb}, {args.hidden}), seq_len {args.seq}, batch {per} per GPU, "
             f"{args.dtype}, {loss}, dropout 0.1, Adam")
 
 
 def cpu_baseline(args):
-    """The CPU oracle (PyTorch-CPU restatement of the reference, fp32) on a bounded
-    sample of the same workload: same model size, seq_len, loss; smaller batch."""
-    import numpy as np
+    """The reference's CPU step (oracle/aten_ref.py: the same ATen modules and loss
+    composition enhanced_two_tower.py / train_enhanced.py run, fp32, pinned to the
+    reference's goldens) on a bounded sample of the workload: same model size, seq_len
+    and loss, BASELINE.md's planned CPU batch (1024), a few timed steps."""
+    import platform
 
-    from oracle import cpu_ref
+    from oracle import aten_ref
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     torch.set_num_threads(threads)
     E, h, T, B = args.emb, args.hidden, args.seq, args.cpu_batch
-    p = {k: v.clone().requires_grad_(True) for k, v in cpu_ref.counter_params(E, h, 0).items()}
-    opt = torch.optim.Adam(list(p.values()))
-    rng = np.random.default_rng(0)
-    table = torch.from_numpy((rng.standard_normal((20000, E)) * 0.1).astype(np.float32))
+    torch.manual_seed(0)
+    model = aten_ref.AtenTwoTower(E, h).train()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    gen = torch.Generator().manual_seed(0)
+    table = torch.randn(20000, E, generator=gen) * 0.1
 
     def batch():
-        ids = torch.from_numpy(rng.integers(0, table.shape[0], (2, B, T)))
-        x = table[ids]
+        ids = torch.randint(0, table.shape[0], (2, B, T), generator=gen)
+        x = table[ids]  # host gather, as EnhancedDataset does per word
         x[:, :, T - max(1, T // 10):] = 0
         return x[0], x[1]
 
     def step():
-        q, d = batch()  # host gather as in EnhancedDataset
+        q, d = batch()
         opt.zero_grad()
-        qv, dv = cpu_ref.forward(q, d, p, drop_p=0.1, seeds=(1, 2))
-        if args.loss == "infonce":
-            loss = cpu_ref.infonce(qv, dv)
-        else:
-            with torch.no_grad():
-                s = cpu_ref.normalize(qv, 1e-8) @ cpu_ref.normalize(dv, 1e-8).t()
-                s.fill_diagonal_(-1.0)
-                idx = s.topk(5, dim=1).indices
-            loss = cpu_ref.margin_loss(qv, dv, dv[idx.reshape(-1)])
+        qv, dv = model(q, d)
+        loss = aten_ref.infonce(qv, dv) if args.loss == "infonce" else aten_ref.hardneg_margin(qv, dv)
         loss.backward()
         opt.step()
 
-    step()  # warm-up
+    for _ in range(args.cpu_warmup):
+        step()
     t0 = time.perf_counter()
     for _ in range(args.cpu_steps):
         step()
     dt = time.perf_counter() - t0
-    return {"value": round(B * args.cpu_steps / dt, 2), "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/cpu_ref.py fp32 train step (fwd+{args.loss}+bwd+Adam), E={E} h={h} T={T}, "
-                      f"batch {B} x {args.cpu_steps} timed steps after 1 warm-up ({dt:.1f} s), "
-                      f"torch {torch.__version__} CPU, {threads} threads"}
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), cpu)
+    except OSError:
+        pass
+    return {"value": round(B * args.cpu_steps / dt, 2), "unit": "pairs/s", "cores": threads, "kind": "reference",
+            "sample": f"reference CPU path (oracle/aten_ref.py: nn.GRU/nn.Linear/nn.LayerNorm + {args.loss} + "
+                      f"torch.optim.Adam, fp32), E={E} h={h} T={T}, batch {B} x {args.cpu_steps} timed steps after "
+                      f"{args.cpu_warmup} warm-up ({dt:.1f} s), torch {torch.__version__} CPU, {threads} threads "
+                      f"on {cpu}"}
 
 
 # HBM traffic per launch of a timing region, from the committed rocprofv3 PMC summary of
@@ -173,10 +185,16 @@ def main():
     from two_towers_amd import dist as tdp
     from two_towers_amd import timing
 
+    if args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 through torch.distributed.run")
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     B, T, h, E, V = args.batch, args.seq, args.hidden, args.emb, args.vocab
+    if args.scaling == "strong":
+        if B % world:
+            raise SystemExit(f"--scaling strong: global batch {B} not divisible by {world} GPUs")
+        B //= world
     torch.manual_seed(1234)  # same weights on every rank
-    model = tta.EnhancedTwoTowerModel(E, h).to(dev).set_compute_dtype(dt).train()
+    model = tta.EnhancedTwoTowerModel(E, h).to(dev).set_compute_dtype(dt).set_process_group(group).train()
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     table = (torch.randn(V, E, device=dev, generator=gen) * 0.1).to(dt)  # Word2Vec-shaped, resident in HBM
     model.set_embedding_table(table)
@@ -202,7 +220,7 @@ def main():
 
     for i in range(args.warmup):
         loss = step(i)
-    first_loss = float(loss) if args.warmup else float("nan")
+    first_loss = float(loss.detach()) if args.warmup else float("nan")
     if world > 1:
         tdist.barrier()
     torch.cuda.synchronize()
@@ -217,7 +235,7 @@ def main():
     elapsed = time.perf_counter() - t0
     timing.enabled = False
     kt = timing.summary()
-    final_loss = float(loss)
+    final_loss = float(loss.detach())
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
@@ -268,7 +286,7 @@ def main():
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True, "scaling": "weak",
+            "warmup": args.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True, "scaling": args.scaling,
             "vs_baseline": None, "dtype": args.dtype,
             "data": f"synthetic: uniform token ids over a {V}x{E} Word2Vec-shaped table resident in HBM, "
                     f"10% pad tail per row, random-init weights (torch seed 1234)",

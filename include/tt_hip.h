@@ -34,10 +34,18 @@ extern "C" {
 #define TT_DT_F32 0
 #define TT_DT_BF16 1
 
-/* Library version string, e.g. "tt_hip 0.1.0 gfx950". */
+/* Library version string, e.g. "tt_hip 0.2.0 gfx950". */
 const char* tt_version(void);
 /* Message describing the last non-zero return on this thread ("" if none). */
 const char* tt_last_error(void);
+/* Kernel-variant switches (process-wide; initialised once from the environment variable
+ * of the same name in upper case with a TT_ prefix, e.g. gru_step <- TT_GRU_STEP):
+ * gru_step, gru_depth, gru_stagger, gru_bwd_rows, gru_bwd_big, gru_bwd_streams,
+ * gemm_persist, gemm_regstage, gemm_stream_out, hn_gemm. Every variant computes the
+ * same function; they exist for A/B measurement and for tests that compare variants.
+ * Not synchronised with launches in flight: set them between steps. */
+int tt_set_option(const char* name, int value);
+int tt_get_option(const char* name, int* value);
 
 /* ---------------------------------------------------------------- featurisation */
 /* Word2Vec row gather: out[i, :] = table[ids[i], :] for ids[i] >= 0, zero row for
@@ -82,6 +90,8 @@ typedef struct {
    * r|z columns live in the dL/dgx buffer, without a copy. */
   const void* a_hi[4];
   int a_split;
+  /* dropout (drop_p > 0): the mask of element (m, n) is keep(drop_seed, drop_row0 + m, n) */
+  uint32_t drop_row0;
 } tt_gemm_batch;
 
 int tt_gemm(int dtype, int out_dtype, int a_kouter, int b_kouter, int m, int n, int k,
@@ -111,6 +121,10 @@ typedef struct {
   int dir;             /* 0: t = 0..T-1 ; 1: t = T-1..0                              */
   uint32_t drop_seed;  /* dropout stream of x1                                       */
   int drop_col0;       /* column of this recurrence inside the layer output (dir*H)  */
+  uint32_t drop_row0;  /* mask row of local row 0: the mask of element (b, t, col) is
+                          keep(drop_seed, drop_row0 + b*T + t, drop_col0 + col), so a
+                          data-parallel rank passes rank * B * T and draws the masks the
+                          single-process run of the global batch would               */
 } tt_gru_fwd_rec;
 
 int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B, int T, int H, long ldg,
@@ -225,11 +239,13 @@ int tt_infonce_fwd(int dtype, const void* qn, long bq, const void* dn, long nd, 
                    float inv_tau, float offdiag_sub, long label_offset, float* lse,
                    float* row_loss, void* ws, void* stream);
 long tt_infonce_fwd_ws_size(long bq, long nd);
-/* Gradient of gscale * sum_i row_loss[i]: dqn [bq,h], ddn [nd,h] (fp32, overwritten).
+/* Gradient of g * sum_i row_loss[i]: dqn [bq,h], ddn [nd,h] (fp32, overwritten).
+ * gscale: DEVICE pointer to the fp32 upstream gradient g (autograd's grad_output, read
+ * by the kernels so the backward never waits on the host), or NULL for g = 1.
  * ws: tt_infonce_bwd_ws_size bytes. */
 int tt_infonce_bwd(int dtype, const void* qn, long bq, const void* dn, long nd, int h,
                    float inv_tau, float offdiag_sub, long label_offset, const float* lse,
-                   float gscale, float* dqn, float* ddn, void* ws, void* stream);
+                   const float* gscale, float* dqn, float* ddn, void* ws, void* stream);
 long tt_infonce_bwd_ws_size(int dtype, long bq, long nd, int h);
 
 /* Hard-negative mining, batched over rows (get_hard_negatives,
@@ -260,12 +276,12 @@ long tt_search_ws_size(int dtype, long Q, long N, int h, int k);
  * row_loss_i = max(margin - pos_i + negm_i, 0). Negatives are rows of dn. */
 int tt_margin_fwd(const float* qn, long bq, const float* dn, long nd, int h, long label_offset,
                   const int32_t* idx, int k, float margin, float* row_loss, void* stream);
-/* Gradient of gscale * sum_i row_loss_i: dqn (overwritten), ddn (accumulated; the
- * caller zeroes it). ws: tt_margin_bwd_ws_size bytes (8 per row) or NULL; with it and
+/* Gradient of g * sum_i row_loss_i: dqn (overwritten), ddn (accumulated; the caller
+ * zeroes it). gscale: device pointer to g (as tt_infonce_bwd) or NULL for 1. ws: tt_margin_bwd_ws_size bytes (8 per row) or NULL; with it and
  * h <= 512, 64 (k + 1) <= 2048, repeated negatives are summed per 64-row group before
  * the atomics into ddn (hard negatives are shared by many rows). */
 int tt_margin_bwd(const float* qn, long bq, const float* dn, long nd, int h, long label_offset,
-                  const int32_t* idx, int k, float margin, float gscale, float* dqn, float* ddn,
+                  const int32_t* idx, int k, float margin, const float* gscale, float* dqn, float* ddn,
                   void* ws, void* stream);
 long tt_margin_bwd_ws_size(long bq);
 

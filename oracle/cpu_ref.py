@@ -54,12 +54,13 @@ def tt_hash3(seed: int, row: np.ndarray, col: np.ndarray) -> np.ndarray:
     return h
 
 
-def dropout_mask(seed: int, rows: int, cols: int, p: float) -> np.ndarray:
-    """Multiplier (0 or 1/(1-p)) for element (row, col); row = b*T + t, col in [0, 2H)."""
+def dropout_mask(seed: int, rows: int, cols: int, p: float, row0: int = 0) -> np.ndarray:
+    """Multiplier (0 or 1/(1-p)) for element (row, col); row = row0 + b*T + t, col in
+    [0, 2H). row0 = rank * B * T on a data-parallel rank (tt_gru_fwd_rec.drop_row0)."""
     if p <= 0.0:
         return np.ones((rows, cols), dtype=np.float32)
     thresh = np.uint64(int(p * 16777216.0 + 0.5))
-    r = np.arange(rows, dtype=np.uint64)[:, None]
+    r = np.arange(row0, row0 + rows, dtype=np.uint64)[:, None]
     c = np.arange(cols, dtype=np.uint64)[None, :]
     keep = (tt_hash3(seed, r, c) >> np.uint64(8)) >= thresh
     return np.where(keep, np.float32(1.0 / (1.0 - p)), np.float32(0.0)).astype(np.float32)

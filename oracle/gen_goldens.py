@@ -251,6 +251,40 @@ def gen_dp(et):
     np.savez_compressed(os.path.join(OUT, "dp_equiv.npz"), **out)
 
 
+def gen_dp_step(et):
+    """One full train_enhanced.py step (train_enhanced.py:58-63) on a global batch of 256,
+    single process, for both losses the bench runs: InfoNCE, and the config-3
+    composition (looped get_hard_negatives over the whole batch + MarginRankingLoss with
+    those negatives). Loss, every parameter gradient and the weights after one
+    Adam(lr=1e-3) step: an N-rank data-parallel step over the same 256 rows must
+    reproduce them. Eval mode: the reference's dropout RNG is
+    not reproducible by another backend."""
+    g = torch.Generator().manual_seed(18)
+    q = torch.randn(256, 6, 16, generator=g)
+    d = torch.randn(256, 6, 16, generator=g)
+    out = {"q": q.numpy(), "d": d.numpy()}
+    for name in ("infonce", "hardneg"):
+        torch.manual_seed(5)
+        model = et.EnhancedTwoTowerModel(16, 8).eval()
+        if name == "infonce":
+            out.update(sd_arrays("w.", model.state_dict()))
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+        opt.zero_grad()
+        qv, dv = model(q, d)
+        if name == "infonce":
+            loss = et.InfoNCELoss()(qv, dv)
+        else:
+            idx = torch.stack([et.get_hard_negatives(qv[i].detach(), dv.detach(), i, 5) for i in range(256)])
+            loss = et.MarginRankingLoss()(qv, dv, dv[idx.reshape(-1)])
+            out["hardneg.idx"] = idx.numpy()
+        loss.backward()
+        out[f"{name}.loss"] = np.float32(loss.item())
+        out.update({f"{name}.g.{k}": p.grad.numpy().copy() for k, p in model.named_parameters()})
+        opt.step()
+        out.update(sd_arrays(f"{name}.w1.", model.state_dict()))
+    np.savez_compressed(os.path.join(OUT, "dp_step.npz"), **out)
+
+
 def import_margin_reference():
     sys.path.insert(0, REF)
     import margin_two_tower as mt  # noqa: E402  (torch / numpy / re only)
@@ -315,6 +349,8 @@ def main():
     if only:  # e.g. `gen_goldens.py margin` regenerates just those fixtures
         if "margin" in only:
             gen_margin(import_margin_reference())
+        if "dp_step" in only:
+            gen_dp_step(import_reference())
         return
     et = import_reference()
     gen_margin(import_margin_reference())
@@ -323,6 +359,7 @@ def main():
     gen_featurize(et)
     gen_losses(et)
     gen_dp(et)
+    gen_dp_step(et)
     gen_mrr(et)
     gen_full(et, 300, 256, 64, 32, "full_h256_t64", 21)
     gen_full(et, 300, 512, 128, 8, "full_h512_t128", 22)

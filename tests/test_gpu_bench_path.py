@@ -1,0 +1,118 @@
+"""Parity of the configuration bench.py measures against the fp32 CPU oracle.
+
+BASELINE configs[2] runs EnhancedTwoTowerModel(300, 256) (GRU H = 512 per direction),
+seq_len 64, bf16, dropout 0.1, hard-negative mining k = 5 + MarginRankingLoss(0.2).
+These tests run exactly the kernels that step runs -- the persistent bf16 GRU forward
+(gru_fwd_seq<4, 8>), the 256x256 BPTT step kernel (gru_bwd_big), the persistent
+input-projection GEMMs, the fp32 head -- at a batch the oracle finishes in seconds, and
+compare with oracle/cpu_ref.py (reference enhanced_two_tower.py:50-65, :67-82, :84-133)
+evaluated in fp32 on the same bf16-rounded weights and inputs, so only the kernels'
+internal bf16 rounding (operands of every MFMA, the saved pre-activations, the bf16
+BPTT carry over 64 steps) is measured.
+
+Tolerances, stated here and asserted below:
+  * loss: relative error <= 2e-3;
+  * tower outputs: max-abs error <= 3e-2 of the largest entry;
+  * every one of the 44 parameter gradients: cosine similarity >= 0.998 and
+    ||g - g_ref|| <= 0.06 ||g_ref||;
+  * hard negatives in bf16 vs the fp32 oracle at B = 1024: >= 97 % of the rows pick the
+    same set of k indices, every differing pick is a near-tie (its fp32 cosine within
+    4e-3 of the oracle's k-th best), and the loss on the picked indices equals the fp32
+    margin loss on those indices to 1e-5.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import two_towers_amd as tta  # noqa: E402
+from oracle import cpu_ref  # noqa: E402
+from two_towers_amd import _lib  # noqa: E402
+
+DEV = "cuda"
+E, HID, T, B = 300, 256, 64, 256  # GRU H = 2 * HID = 512
+
+
+def _bf16(x):
+    return x.to(torch.bfloat16).float()
+
+
+def _model(seed):
+    torch.manual_seed(seed)
+    m = tta.EnhancedTwoTowerModel(E, HID)
+    with torch.no_grad():
+        for prm in m.parameters():
+            prm.copy_(_bf16(prm))
+    p = {k: v.detach().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    return m.to(DEV).set_compute_dtype(torch.bfloat16), p
+
+
+def _grad_check(named, ref):
+    worst = []
+    for k, pr in ref.items():
+        a, b = named[k].grad.double().cpu(), pr.grad.double()
+        cos = float((a * b).sum() / (a.norm() * b.norm() + 1e-300))
+        frob = float((a - b).norm() / (b.norm() + 1e-300))
+        worst.append((frob, cos, k))
+        assert cos >= 0.998 and frob <= 0.06, (k, cos, frob)
+    return max(worst)
+
+
+@pytest.mark.parametrize("drop_p", [0.0, 0.1])
+def test_bench_config_bf16_matches_oracle(drop_p):
+    lib = _lib.load()
+    assert lib.tt_gru_fwd_launches(_lib.DT_BF16, T, 2 * HID) == 1, "persistent forward expected at H=512"
+    m, p = _model(31)
+    m.train() if drop_p > 0 else m.eval()
+    g = torch.Generator().manual_seed(32)
+    q = _bf16(torch.randn(B, T, E, generator=g) * 0.5)
+    d = _bf16(torch.randn(B, T, E, generator=g) * 0.5)
+    torch.manual_seed(33)  # the forward draws one dropout seed per tower from this stream
+    qv, dv = m(q.to(DEV), d.to(DEV))
+    loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
+    loss.backward()
+    torch.manual_seed(33)
+    seeds = [int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) for _ in range(2)] if drop_p > 0 else [0, 0]
+    rq, rd = cpu_ref.forward(q, d, p, drop_p=drop_p, seeds=seeds)
+    rl = cpu_ref.infonce(rq, rd)
+    rl.backward()
+    lv, rv = float(loss.detach()), float(rl.detach())
+    assert abs(lv - rv) <= 2e-3 * abs(rv), (lv, rv)
+    for a, b in ((qv, rq), (dv, rd)):
+        a, b = a.detach().double().cpu(), b.detach().double()
+        assert float((a - b).abs().max() / b.abs().max()) <= 3e-2
+    frob, cos, k = _grad_check(dict(m.named_parameters()), p)
+    print(f"drop {drop_p}: loss {lv:.6f} vs {rv:.6f}; worst gradient {k}: rel {frob:.4f}, cos {cos:.5f}")
+
+
+def test_hardneg_margin_bf16_b1024_agrees_with_fp32():
+    Bq, h, k = 1024, 256, 5
+    g = torch.Generator().manual_seed(34)
+    d = torch.randn(Bq, h, generator=g)
+    q = d + 4.0 * torch.randn(Bq, h, generator=g)  # pos cos ~0.24, top negatives ~0.2: hinges active
+    qd, dd = q.clone().to(DEV).requires_grad_(True), d.clone().to(DEV).requires_grad_(True)
+    crit = tta.HardNegativeMarginLoss(k=k, margin=0.2, compute_dtype=torch.bfloat16)
+    loss = crit(qd, dd)
+    loss.backward()
+    idx = crit.last_indices.long().cpu()
+    _, ridx = cpu_ref.hardneg_margin(q.clone(), d.clone(), k, 0.2)
+    same = np.array([set(idx[i].tolist()) == set(ridx[i].tolist()) for i in range(Bq)])
+    assert same.mean() >= 0.97, same.mean()
+    # every disagreement is a near-tie of the fp32 ranking
+    cos = cpu_ref.normalize(q, 1e-8) @ cpu_ref.normalize(d, 1e-8).t()
+    cos.fill_diagonal_(-1.0)
+    kth = cos.gather(1, ridx)[:, -1]
+    for i in np.nonzero(~same)[0]:
+        for j in set(idx[i].tolist()) - set(ridx[i].tolist()):
+            assert float(kth[i] - cos[i, j]) <= 4e-3, (i, j, float(kth[i]), float(cos[i, j]))
+    # given the picked indices, the loss and its gradients are the fp32 margin loss
+    qr, dr = q.clone().requires_grad_(True), d.clone().requires_grad_(True)
+    rl = cpu_ref.margin_loss(qr, dr, dr[idx.reshape(-1)], 0.2)
+    rl.backward()
+    assert float(rl.detach()) > 0.01, "hinges inactive: the test would compare zeros"
+    assert abs(float(loss.detach()) - float(rl.detach())) <= 1e-5
+    for a, b in ((qd.grad, qr.grad), (dd.grad, dr.grad)):
+        a, b = a.double().cpu(), b.double()
+        assert float((a - b).abs().max() / b.abs().max()) <= 1e-4
+    print(f"hard negatives: {same.mean():.4f} of rows pick the fp32 set; loss {float(loss):.6f}")

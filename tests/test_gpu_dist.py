@@ -97,3 +97,144 @@ def test_two_ranks_match_single_process(kind):
         if idx is not None:
             ref_idx = crit.last_indices.cpu().numpy()[r * B:(r + 1) * B]
             assert (idx == ref_idx).all()
+
+
+# ------------------------------------------------------------------ full training step
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _dp_golden():
+    import numpy as np
+    return np.load(os.path.join(GOLD, "dp_step.npz"), allow_pickle=False)
+
+
+def _dp_model(z):
+    import two_towers_amd as tta
+    m = tta.EnhancedTwoTowerModel(16, 8)
+    m.load_state_dict({k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w.")})
+    return m.cuda().eval()
+
+
+def _step_rank(rank, world, port, kind, out):
+    """train_enhanced.py:58-63 on this rank's rows: zero_grad, forward, loss (global
+    negative pool), backward, gradient all-reduce, Adam."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import two_towers_amd as tta
+        from two_towers_amd import dist as tdp
+        z = _dp_golden()
+        n = z["q"].shape[0] // world
+        q = torch.from_numpy(z["q"][rank * n:(rank + 1) * n]).cuda()
+        d = torch.from_numpy(z["d"][rank * n:(rank + 1) * n]).cuda()
+        m = _dp_model(z)
+        opt = tta.Adam(m.parameters(), lr=1e-3)
+        crit = tta.InfoNCELoss() if kind == "infonce" else tta.HardNegativeMarginLoss(k=5, margin=0.2)
+        opt.zero_grad()
+        loss = crit(*m(q, d))
+        loss.backward()
+        tdp.allreduce_grads(list(m.parameters()))
+        grads = {k: p.grad.cpu().numpy().copy() for k, p in m.named_parameters()}
+        opt.step()
+        w1 = {k: v.cpu().numpy().copy() for k, v in m.state_dict().items()}
+        idx = getattr(crit, "last_indices", None)
+        out.put((rank, float(loss.detach()), grads, w1, None if idx is None else idx.cpu().numpy().copy()))
+        torch.distributed.barrier()
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["infonce", "hardneg"])
+def test_two_rank_train_step_matches_reference_global_batch(kind):
+    """a world-2 data-parallel step over the 256 rows of
+    dp_step.npz (128 per rank) reproduces the reference's single-process step on all 256:
+    loss 1e-5 relative, every all-reduced gradient 2e-3 (max-abs over max, the fp32
+    tolerance of the golden tests), weights after Adam within 1 % of lr, and the mined
+    hard negatives of each rank equal the reference's rows."""
+    import numpy as np
+    z = _dp_golden()
+    ctx = mp.get_context("spawn")
+    out = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_step_rank, args=(r, 2, port, kind, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r = out.get(timeout=120)
+        res[r[0]] = r[1:]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        loss, grads, w1, idx = res[r]
+        ref = float(z[f"{kind}.loss"])
+        assert abs(loss - ref) <= 1e-5 * abs(ref), (r, loss, ref)
+        for k, g in grads.items():
+            gr = z[f"{kind}.g.{k}"]
+            assert float(np.abs(g - gr).max()) <= 2e-3 * float(np.abs(gr).max()) + 1e-9, (r, k)
+        for k, w in w1.items():
+            assert float(np.abs(w - z[f"{kind}.w1.{k}"]).max()) <= 1e-5, (r, k)
+        if idx is not None:
+            assert (idx == z["hardneg.idx"][r * 128:(r + 1) * 128]).all()
+
+
+def _drop_rank(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import two_towers_amd as tta
+        from two_towers_amd import dist as tdp
+        z = _dp_golden()
+        n = z["q"].shape[0] // world
+        m = _dp_model(z).train()  # GRU dropout 0.1 between the layers
+        torch.manual_seed(40)  # same dropout seeds on every rank, as in bench.py / train.py
+        qv, dv = m(torch.from_numpy(z["q"][rank * n:(rank + 1) * n]).cuda(),
+                   torch.from_numpy(z["d"][rank * n:(rank + 1) * n]).cuda())
+        tta.InfoNCELoss()(qv, dv).backward()
+        tdp.allreduce_grads(list(m.parameters()))
+        out.put((rank, qv.detach().cpu().numpy().copy(),
+                 {k: p.grad.cpu().numpy().copy() for k, p in m.named_parameters()}))
+        torch.distributed.barrier()
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_two_rank_dropout_masks_are_global_batch_masks():
+    """With dropout on, rank r's rows draw the masks of global rows r*B_l.. (mask row
+    offset rank * B_l * T, tt_gru_fwd_rec.drop_row0): the two ranks never repeat each
+    other's masks, and their outputs and summed gradients equal the single-process
+    train-mode step on the whole batch with the same seeds."""
+    import numpy as np
+
+    import two_towers_amd as tta
+    z = _dp_golden()
+    ctx = mp.get_context("spawn")
+    out = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_drop_rank, args=(r, 2, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r = out.get(timeout=120)
+        res[r[0]] = r[1:]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    m = _dp_model(z).train()
+    torch.manual_seed(40)
+    qv, dv = m(torch.from_numpy(z["q"]).cuda(), torch.from_numpy(z["d"]).cuda())
+    tta.InfoNCELoss()(qv, dv).backward()
+    q1 = qv.detach().cpu().numpy()
+    n = q1.shape[0] // 2
+    for r in range(2):
+        np.testing.assert_allclose(res[r][0], q1[r * n:(r + 1) * n], rtol=0, atol=1e-5 * np.abs(q1).max())
+    for k, p in m.named_parameters():
+        g = p.grad.cpu().numpy()
+        for r in range(2):
+            assert float(np.abs(res[r][1][k] - g).max()) <= 1e-4 * float(np.abs(g).max()) + 1e-9, (r, k)
+    # the eval outputs differ from the train outputs: dropout really ran
+    with torch.no_grad():
+        qe, _ = m.eval()(torch.from_numpy(z["q"]).cuda(), torch.from_numpy(z["d"]).cuda())
+    assert float((qe.cpu() - torch.from_numpy(q1)).abs().max()) > 1e-4

@@ -11,7 +11,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 from two_towers_amd import _lib  # noqa: E402
-from two_towers_amd._lib import call, dtype_code  # noqa: E402
+from two_towers_amd._lib import call, dtype_code, option  # noqa: E402
 
 DEV = "cuda"
 
@@ -103,7 +103,7 @@ def test_hardneg_bench_size_consistent():
 
 
 @pytest.mark.parametrize("B,nd,h,lab", [(1000, 3000, 256, 0), (300, 4100, 128, -1), (8192, 8192, 256, 0)])
-def test_hardneg_scan_matches_gemm_path(monkeypatch, B, nd, h, lab):
+def test_hardneg_scan_matches_gemm_path(B, nd, h, lab):
     """Random (non-integer) normalised bf16 rows: the streamed scan and the GEMM + split
     top-k path form every score with the same MFMA instruction and k order, so indices
     and values agree bit-exactly -- including near-ties, which a rescoring that differed
@@ -112,8 +112,8 @@ def test_hardneg_scan_matches_gemm_path(monkeypatch, B, nd, h, lab):
     q = torch.nn.functional.normalize(torch.randn(B, h, generator=g), dim=1)
     d = torch.nn.functional.normalize(torch.randn(nd, h, generator=g), dim=1)
     si, sv = run_hardneg(q, d, lab, 5, torch.bfloat16)
-    monkeypatch.setenv("TT_HN_GEMM", "1")
-    gi, gv = run_hardneg(q, d, lab, 5, torch.bfloat16)
+    with option("hn_gemm", 1):
+        gi, gv = run_hardneg(q, d, lab, 5, torch.bfloat16)
     assert torch.equal(sv, gv)
     assert torch.equal(si, gi)
 
@@ -130,12 +130,8 @@ def test_hardneg_hot_chunks():
     d[:64] = torch.nn.functional.normalize(base + 0.05 * torch.randn(64, h, generator=g), dim=1)
     d = d.bfloat16().float()
     si, sv = run_hardneg(q, d, 0, k, torch.bfloat16)
-    import os
-    os.environ["TT_HN_GEMM"] = "1"
-    try:
+    with option("hn_gemm", 1):
         gi, gv = run_hardneg(q, d, 0, k, torch.bfloat16)
-    finally:
-        del os.environ["TT_HN_GEMM"]
     assert torch.equal(sv, gv) and torch.equal(si, gi)
     assert bool((si < 64).all())
 
@@ -168,11 +164,12 @@ def test_margin_bwd_repeated_negatives(B, nd, h, k, lab, hot):
     margin, gscale = 2.0, 1.0 / B  # margin 2: every row active
     rq, rd = ref_margin_grads(q, d, lab, idx, margin, gscale)
     qd, dd, idd = q.to(DEV), d.to(DEV), idx.to(DEV)
+    gdev = torch.tensor([gscale], dtype=torch.float32, device=DEV)  # device-side upstream gradient
     dq = torch.empty(B, h, device=DEV)
     for use_ws in (True, False):  # grouped kernels / per-row atomic kernel
         ddn = torch.zeros(nd, h, device=DEV)
         ws = torch.empty(_lib.load().tt_margin_bwd_ws_size(B), dtype=torch.uint8, device=DEV)
-        call("tt_margin_bwd", qd.data_ptr(), B, dd.data_ptr(), nd, h, lab, idd.data_ptr(), k, margin, gscale,
+        call("tt_margin_bwd", qd.data_ptr(), B, dd.data_ptr(), nd, h, lab, idd.data_ptr(), k, margin, gdev.data_ptr(),
              dq.data_ptr(), ddn.data_ptr(), ws.data_ptr() if use_ws else None, torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         assert (dq.cpu().double() - rq).abs().max() < 1e-6

@@ -6,6 +6,7 @@ pytestmark = pytest.mark.gpu
 
 import two_towers_amd as tta  # noqa: E402
 from oracle import cpu_ref  # noqa: E402
+from two_towers_amd._lib import option  # noqa: E402
 
 DEV = "cuda"
 
@@ -150,8 +151,8 @@ def test_cpu_tensors_fail_loudly():
 
 
 @pytest.mark.parametrize("h,B,T", [(128, 1100, 4), (256, 2048, 3)])
-def test_persistent_gru_staggered_block_order(h, B, T, monkeypatch):
-    """TT_GRU_STAGGER=1 (H 256 / 512 instances): each workgroup starts its unit-block
+def test_persistent_gru_staggered_block_order(h, B, T):
+    """Option gru_stagger = 1 (H 256 / 512 instances): each workgroup starts its unit-block
     loop at (blockIdx / 8) mod nblk; same arithmetic per unit, so outputs and gradients
     agree with the default order to fp32 rounding. B >= 1100 gives every offset."""
     E = 48
@@ -159,13 +160,13 @@ def test_persistent_gru_staggered_block_order(h, B, T, monkeypatch):
     q = torch.randn(B, T, E, generator=g).to(DEV)
     d = torch.randn(B, T, E, generator=g).to(DEV)
     outs = []
-    for stg in ("0", "1"):
-        monkeypatch.setenv("TT_GRU_STAGGER", stg)
+    for stg in (0, 1):
         m, _ = make_model(E, h, 3)
         m = m.to(DEV).train().set_compute_dtype(torch.bfloat16)
-        qv, dv = m(q, d)
-        loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
-        loss.backward()
+        with option("gru_stagger", stg):
+            qv, dv = m(q, d)
+            loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
+            loss.backward()
         outs.append((qv.detach().clone(), dv.detach().clone(), {k: p.grad.clone() for k, p in m.named_parameters()}))
     (q0, d0, g0), (q1, d1, g1) = outs
     assert rel(q1, q0) < 1e-5 and rel(d1, d0) < 1e-5
@@ -174,22 +175,22 @@ def test_persistent_gru_staggered_block_order(h, B, T, monkeypatch):
 
 
 @pytest.mark.parametrize("h,B,T", [(32, 96, 10), (64, 200, 7), (128, 70, 4), (256, 130, 5)])
-def test_persistent_gru_matches_step_kernel(h, B, T, monkeypatch):
+def test_persistent_gru_matches_step_kernel(h, B, T):
     """bf16 forward + backward through the persistent (row-resident) GRU forward
-    kernel vs the per-step kernel (env TT_GRU_STEP=1): same arithmetic in the same
+    kernel vs the per-step kernel (option gru_step = 1): same arithmetic in the same
     order, so outputs and gradients agree to fp32 rounding of the gate math."""
     E = 48
     g = torch.Generator().manual_seed(11)
     q = torch.randn(B, T, E, generator=g).to(DEV)
     d = torch.randn(B, T, E, generator=g).to(DEV)
     outs = []
-    for step in ("1", "0"):
-        monkeypatch.setenv("TT_GRU_STEP", step)
+    for step in (1, 0):
         m, _ = make_model(E, h, 3)
         m = m.to(DEV).train().set_compute_dtype(torch.bfloat16)
-        qv, dv = m(q, d)
-        loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
-        loss.backward()
+        with option("gru_step", step):
+            qv, dv = m(q, d)
+            loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
+            loss.backward()
         outs.append((qv.detach().clone(), dv.detach().clone(), {k: p.grad.clone() for k, p in m.named_parameters()}))
     (q0, d0, g0), (q1, d1, g1) = outs
     assert rel(q1, q0) < 1e-5 and rel(d1, d0) < 1e-5
@@ -198,21 +199,21 @@ def test_persistent_gru_matches_step_kernel(h, B, T, monkeypatch):
 
 
 @pytest.mark.parametrize("B,T", [(130, 5), (520, 3)])
-def test_big_tile_gru_backward_matches_step_kernel(B, T, monkeypatch):
+def test_big_tile_gru_backward_matches_step_kernel(B, T):
     """bf16 H=512 backward on 256x256 tiles (8-phase GEMM, two-pass epilogue) vs the
-    128x128 step kernels (env TT_GRU_BWD_BIG=0): gradients agree to accumulation order."""
+    128x128 step kernels (option gru_bwd_big = 0): gradients agree to accumulation order."""
     E, h = 40, 256
     g = torch.Generator().manual_seed(12)
     q = torch.randn(B, T, E, generator=g).to(DEV)
     d = torch.randn(B, T, E, generator=g).to(DEV)
     outs = []
-    for big in ("0", "1"):
-        monkeypatch.setenv("TT_GRU_BWD_BIG", big)
+    for big in (0, 1):
         m, _ = make_model(E, h, 4)
         m = m.to(DEV).train().set_compute_dtype(torch.bfloat16)
-        qv, dv = m(q, d)
-        loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
-        loss.backward()
+        with option("gru_bwd_big", big):
+            qv, dv = m(q, d)
+            loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
+            loss.backward()
         outs.append({k: p.grad.clone() for k, p in m.named_parameters()})
     for k in outs[0]:
         a, b = outs[1][k].double(), outs[0][k].double()

@@ -155,3 +155,58 @@ def test_margin_featurize():
     for text, emb in zip(z["texts"], z["emb"]):
         ids = cpu_ref.margin_text_to_ids(str(text), vocab, T)
         np.testing.assert_array_equal(cpu_ref.ids_to_embedding(ids, z["vecs"]), emb)
+
+
+@pytest.mark.parametrize("loss", ["infonce", "hardneg"])
+def test_dp_step(loss):
+    """One full step (loss, 44 gradients, Adam update) of the global batch the DP test
+    splits over ranks: the oracle reproduces the reference run (dp_step.npz)."""
+    z = load("dp_step")
+    p = {k: v.requires_grad_(True) for k, v in params(z, "w.").items()}
+    qv, dv = cpu_ref.forward(torch.from_numpy(z["q"]), torch.from_numpy(z["d"]), p)
+    if loss == "infonce":
+        lv = cpu_ref.infonce(qv, dv)
+    else:
+        lv, idx = cpu_ref.hardneg_margin(qv, dv, 5, 0.2)
+        np.testing.assert_array_equal(idx.numpy(), z["hardneg.idx"])
+    close(float(lv), z[f"{loss}.loss"], rtol=1e-5)
+    opt = torch.optim.Adam(list(p.values()), lr=1e-3)
+    lv.backward()
+    for k, t in p.items():  # max-abs error relative to the largest entry
+        ref = z[f"{loss}.g.{k}"]
+        assert float((t.grad - torch.from_numpy(ref)).abs().max()) <= 1e-4 * float(np.abs(ref).max()) + 1e-9, k
+    opt.step()
+    # Adam's first step is ~lr * sign(g): where |g| is near eps the update is sensitive
+    # to the gradient's last bits, so the weights are compared to 1 % of lr
+    for k, t in p.items():
+        close(t.detach(), z[f"{loss}.w1.{k}"], rtol=0, atol=1e-5)
+
+
+def test_aten_reference_path_matches_goldens():
+    """oracle/aten_ref.py (the reference's ATen modules: nn.GRU, nn.Linear, nn.LayerNorm,
+    the loss compositions) reproduces the reference run: it is the timed CPU baseline."""
+    from oracle import aten_ref
+    z = load("tiny_model")
+    m = aten_ref.AtenTwoTower(16, 8).eval()
+    m.load_state_dict({k: v for k, v in params(z, "w.").items()})
+    qv, dv = m(torch.from_numpy(z["q"]), torch.from_numpy(z["d"]))
+    loss = aten_ref.infonce(qv, dv)
+    loss.backward()
+    close(qv.detach(), z["q_vec"])
+    close(float(loss), z["loss"])
+    for k, p in m.named_parameters():
+        close(p.grad, z[f"g.{k}"], rtol=1e-4, atol=1e-6)
+    z = load("dp_step")
+    m = aten_ref.AtenTwoTower(16, 8).eval()
+    m.load_state_dict({k: v for k, v in params(z, "w.").items()})
+    loss = aten_ref.hardneg_margin(*m(torch.from_numpy(z["q"]), torch.from_numpy(z["d"])))
+    close(float(loss), z["hardneg.loss"], rtol=1e-5)
+
+
+def test_dropout_mask_row_offset_is_a_slice_of_the_global_mask():
+    """A data-parallel rank's mask rows (row0 = rank * B * T) are its slice of the
+    single-process mask of the global batch, and different ranks get different masks."""
+    full = cpu_ref.dropout_mask(1234, 4 * 60, 32, 0.1)
+    for r in range(4):
+        np.testing.assert_array_equal(cpu_ref.dropout_mask(1234, 60, 32, 0.1, row0=r * 60), full[r * 60:(r + 1) * 60])
+    assert not np.array_equal(full[:60], full[60:120])

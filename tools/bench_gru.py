@@ -1,5 +1,5 @@
 """Micro-benchmark of tt_gru_fwd / tt_gru_bwd at the bench shape (4 recurrences:
-2 towers x 2 directions), HIP-event timed. Variants via env (TT_GRU_STEP, TT_GRU_DBG)."""
+2 towers x 2 directions), HIP-event timed. Variants via tt_set_option (and TT_GRU_DBG in a -DTT_DIAG build)."""
 import argparse
 import json
 import os
@@ -9,7 +9,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from two_towers_amd import _lib  # noqa: E402
-from two_towers_amd._lib import GruBwdRec, GruFwdRec, call, stream_ptr  # noqa: E402
+from two_towers_amd._lib import GruBwdRec, GruFwdRec, call, set_option, stream_ptr  # noqa: E402
 
 
 def setup(B, T, H, dev):
@@ -83,9 +83,9 @@ def main():
         if not v:
             continue
         rows, dbg, strm = (v.split(":") + ["0", "2"])[:3]
-        os.environ["TT_GRU_BWD_ROWS"] = rows
-        os.environ["TT_GRU_DBG"] = dbg
-        os.environ["TT_GRU_BWD_STREAMS"] = strm
+        set_option("gru_bwd_rows", int(rows))
+        os.environ["TT_GRU_DBG"] = dbg  # read only by a -DTT_DIAG build
+        set_option("gru_bwd_streams", int(strm))
         brecs, bkeep = setup_bwd(a.B, a.T, a.H, keep, dev)
         f = lambda: call("tt_gru_bwd", 1, brecs, 4, a.B, a.T, a.H, 2 * a.H, 8 * a.H, 2 * a.H, st)
         f()
@@ -103,9 +103,9 @@ def main():
         if not v:
             continue
         kind, dbg, *depth = v.split(":")
-        os.environ["TT_GRU_STEP"] = "1" if kind == "step" else "0"
-        os.environ["TT_GRU_DBG"] = dbg
-        os.environ["TT_GRU_DEPTH"] = depth[0] if depth else "4"
+        set_option("gru_step", 1 if kind == "step" else 0)
+        os.environ["TT_GRU_DBG"] = dbg  # read only by a -DTT_DIAG build
+        set_option("gru_depth", int(depth[0]) if depth else 4)
         f = lambda: call("tt_gru_fwd", 1, recs, 4, a.B, a.T, a.H, 6 * a.H, 2 * a.H, 0.1, st)
         f()
         torch.cuda.synchronize()

@@ -6,7 +6,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tools.bench_gru import setup  # noqa: E402
-from two_towers_amd._lib import call, stream_ptr  # noqa: E402
+from two_towers_amd._lib import call, set_option, stream_ptr  # noqa: E402
 
 for (B, T, H) in [(200, 7, 128), (200, 7, 512), (128, 3, 128)]:
     torch.manual_seed(0)
@@ -14,7 +14,7 @@ for (B, T, H) in [(200, 7, 128), (200, 7, 512), (128, 3, 128)]:
     G, whh, bhn, Y, X1, S, hs = keep
     outs = []
     for step in ("1", "0"):
-        os.environ["TT_GRU_STEP"] = step
+        set_option("gru_step", int(step))
         for y in Y: y.zero_()
         for s2 in S:
             for s in s2: s.zero_()

@@ -5,6 +5,7 @@ fallback: if the library is missing or no ROCm GPU is visible, every op raises.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 from ctypes import POINTER, c_float, c_int, c_long, c_uint32, c_void_p
@@ -32,6 +33,7 @@ class GemmBatch(ctypes.Structure):
         ("bshift", c_int * 4),
         ("a_hi", c_void_p * 4),
         ("a_split", c_int),
+        ("drop_row0", c_uint32),
     ]
 
 
@@ -39,7 +41,7 @@ class GruFwdRec(ctypes.Structure):
     _fields_ = [
         ("g", c_void_p), ("whh", c_void_p), ("bhn", c_void_p), ("y", c_void_p), ("x1", c_void_p),
         ("save", c_void_p), ("hstate", c_void_p), ("dir", c_int), ("drop_seed", c_uint32),
-        ("drop_col0", c_int),
+        ("drop_col0", c_int), ("drop_row0", c_uint32),
     ]
 
 
@@ -87,6 +89,8 @@ class Head1BwdIO(ctypes.Structure):
 _SIGS = {
     "tt_version": (ctypes.c_char_p, []),
     "tt_last_error": (ctypes.c_char_p, []),
+    "tt_set_option": (c_int, [ctypes.c_char_p, c_int]),
+    "tt_get_option": (c_int, [ctypes.c_char_p, POINTER(c_int)]),
     "tt_embed_gather": (c_int, [c_int, c_void_p, c_long, c_int, c_void_p, c_long, c_void_p, c_void_p]),
     "tt_pack_rows": (c_int, [c_int, c_void_p, c_long, c_int, c_int, c_void_p, c_void_p]),
     "tt_cast": (c_int, [c_int, c_void_p, c_long, c_void_p, c_void_p]),
@@ -115,7 +119,7 @@ _SIGS = {
                                c_void_p, c_void_p, c_void_p, c_void_p]),
     "tt_infonce_fwd_ws_size": (c_long, [c_long, c_long]),
     "tt_infonce_bwd": (c_int, [c_int, c_void_p, c_long, c_void_p, c_long, c_int, c_float, c_float, c_long,
-                               c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "tt_infonce_bwd_ws_size": (c_long, [c_int, c_long, c_long, c_int]),
     "tt_hardneg_topk": (c_int, [c_int, c_void_p, c_long, c_void_p, c_long, c_int, c_long, c_int, c_void_p,
                                 c_void_p, c_void_p, c_void_p]),
@@ -126,7 +130,7 @@ _SIGS = {
     "tt_margin_fwd": (c_int, [c_void_p, c_long, c_void_p, c_long, c_int, c_long, c_void_p, c_int, c_float,
                               c_void_p, c_void_p]),
     "tt_margin_bwd": (c_int, [c_void_p, c_long, c_void_p, c_long, c_int, c_long, c_void_p, c_int, c_float,
-                              c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "tt_margin_bwd_ws_size": (c_long, [c_long]),
     "tt_sum": (c_int, [c_void_p, c_long, c_float, c_void_p, c_void_p]),
     "tt_adam_multi": (c_int, [POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p),
@@ -169,6 +173,31 @@ def check(rc: int, what: str = ""):
 def call(name: str, *args):
     lib = load()
     check(getattr(lib, name)(*args), name)
+
+
+def get_option(name: str) -> int:
+    v = c_int(0)
+    call("tt_get_option", name.encode(), ctypes.byref(v))
+    return v.value
+
+
+def set_option(name: str, value: int) -> int:
+    """Select a kernel variant (tt_set_option); returns the previous value."""
+    old = get_option(name)
+    call("tt_set_option", name.encode(), int(value))
+    return old
+
+
+@contextlib.contextmanager
+def option(name: str, value: int):
+    """with option("gru_step", 1): ...  -- a variant for the duration of the block."""
+    torch.cuda.synchronize()
+    old = set_option(name, value)
+    try:
+        yield
+    finally:
+        torch.cuda.synchronize()
+        set_option(name, old)
 
 
 def ptr(t: torch.Tensor | None) -> int | None:

@@ -8,6 +8,24 @@
 
 namespace tt {
 void set_error(const char* fmt, ...);
+
+// Kernel-variant switches. Read once from the environment (TT_GRU_STEP, ...) when the
+// library is first used, changed only through tt_set_option(): nothing on a launch
+// path calls getenv.
+enum Opt {
+  OPT_GRU_STEP,         // 1: per-step GRU forward even where the persistent kernel applies
+  OPT_GRU_DEPTH,        // persistent forward W_hh ring depth cap (1, 2, 4)
+  OPT_GRU_STAGGER,      // persistent forward: staggered W_hh block order (fixed-NKT instances)
+  OPT_GRU_BWD_ROWS,     // 128 or 64 batch rows per backward step tile
+  OPT_GRU_BWD_BIG,      // 0: 128x128 backward step kernels instead of 256x256
+  OPT_GRU_BWD_STREAMS,  // 1: one stream chain for the 128x128 backward
+  OPT_GEMM_PERSIST,     // 0: no persistent short-K GEMM
+  OPT_GEMM_REGSTAGE,    // 1/2: force register staging / 128-tiles (9: no epilogue, timing)
+  OPT_GEMM_STREAM_OUT,  // 0: no write-through output stores
+  OPT_HN_GEMM,          // 1: hard-negative top-k through GEMM + split top-k, no scan
+  OPT_N
+};
+int opt(Opt o);
 }  // namespace tt
 
 #define TT_CHECK_ARG(cond, ...)            \

@@ -3,6 +3,7 @@
 #include <stdarg.h>
 #include <stdlib.h>
 
+#include <atomic>
 #include <type_traits>
 
 #include "tt_api.h"
@@ -18,8 +19,56 @@ void set_error(const char* fmt, ...) {
 }
 }  // namespace tt
 
-extern "C" const char* tt_version(void) { return "tt_hip 0.1.0 gfx950"; }
+namespace tt {
+namespace {
+struct OptDef {
+  const char* name;
+  const char* env;
+  int dflt;
+};
+constexpr OptDef kOpts[OPT_N] = {
+    {"gru_step", "TT_GRU_STEP", 0},         {"gru_depth", "TT_GRU_DEPTH", 4},
+    {"gru_stagger", "TT_GRU_STAGGER", 0},   {"gru_bwd_rows", "TT_GRU_BWD_ROWS", 128},
+    {"gru_bwd_big", "TT_GRU_BWD_BIG", 1},   {"gru_bwd_streams", "TT_GRU_BWD_STREAMS", 2},
+    {"gemm_persist", "TT_GEMM_PERSIST", 1}, {"gemm_regstage", "TT_GEMM_REGSTAGE", 0},
+    {"gemm_stream_out", "TT_GEMM_STREAM_OUT", 1}, {"hn_gemm", "TT_HN_GEMM", 0},
+};
+struct OptTable {
+  std::atomic<int> v[OPT_N];
+  OptTable() {
+    for (int i = 0; i < OPT_N; ++i) {
+      const char* e = getenv(kOpts[i].env);
+      v[i].store(e && *e ? atoi(e) : kOpts[i].dflt, std::memory_order_relaxed);
+    }
+  }
+};
+OptTable& opts() {
+  static OptTable t;  // thread-safe one-time init
+  return t;
+}
+int find_opt(const char* name) {
+  for (int i = 0; name && i < OPT_N; ++i)
+    if (strcmp(name, kOpts[i].name) == 0) return i;
+  return -1;
+}
+}  // namespace
+int opt(Opt o) { return opts().v[o].load(std::memory_order_relaxed); }
+}  // namespace tt
+
+extern "C" const char* tt_version(void) { return "tt_hip 0.2.0 gfx950"; }
 extern "C" const char* tt_last_error(void) { return tt::g_err; }
+extern "C" int tt_set_option(const char* name, int value) {
+  const int i = tt::find_opt(name);
+  TT_CHECK_ARG(i >= 0, "tt_set_option: unknown option '%s'", name ? name : "(null)");
+  tt::opts().v[i].store(value, std::memory_order_relaxed);
+  return 0;
+}
+extern "C" int tt_get_option(const char* name, int* value) {
+  const int i = tt::find_opt(name);
+  TT_CHECK_ARG(i >= 0 && value, "tt_get_option: unknown option '%s'", name ? name : "(null)");
+  *value = tt::opt((tt::Opt)i);
+  return 0;
+}
 
 namespace {
 
@@ -36,14 +85,13 @@ struct GemmArgs {
   int splits, kt_per_split;
   float alpha;
   int beta, relu, seq_t;
-  uint32_t drop_seed, drop_thresh;
+  uint32_t drop_seed, drop_thresh, drop_row0;
   float drop_inv_keep;
   long part_stride;  // elements between split partials (fp32), 0 if no split
   int vec_ok;        // C rows 16-byte aligned: 8-column vector stores allowed
   int force_regstage;
   int bias_vec_ok;  // every bias pointer 16-byte aligned
   int stream_out;   // write-through (sc1) output stores: big outputs
-  int dbg;          // timing diagnostics (env TT_GEMM_DBG): 1 = persistent epilogue issues no stores
 };
 
 constexpr int BM = 128, BN = 128;  // tile of the register-staged / small path
@@ -109,10 +157,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_kernel(GemmArgs g) {
     run(ttg::KCPlain<T>{A, g.lda, m0, g.M});
   }
 
-  if (g.force_regstage == 9) {  // timing diagnostics only: main loop without epilogue
+#ifdef TT_DIAG
+  if (g.force_regstage == 9) {  // diagnostic build only: main loop without epilogue
     if (threadIdx.x == 0 && acc[0][0][0] == 12345.f) static_cast<float*>(g.c[bi])[0] = 1.f;
     return;
   }
+#endif
   // ---- epilogue: stage 64-row slices of the fp32 tile in LDS, then every thread
   // finishes 8 consecutive columns of a row and writes them with 16-byte stores.
   const bool partial = g.splits > 1;
@@ -170,7 +220,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_kernel(GemmArgs g) {
           for (int e = 0; e < 8; ++e) {
             float x = v[e] * g.alpha + bv[e];
             if (g.relu) x = fmaxf(x, 0.f);
-            if (g.drop_thresh) x *= tt_dropout_scale(g.drop_seed, gm, gn + e, g.drop_thresh, g.drop_inv_keep);
+            if (g.drop_thresh) x *= tt_dropout_scale(g.drop_seed, g.drop_row0 + (uint32_t)gm, gn + e, g.drop_thresh, g.drop_inv_keep);
             v[e] = x;
           }
           TO* dst = C + (long)gm * ldc + gn;
@@ -377,12 +427,11 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
           for (int e = 0; e < 8; ++e) {
             float x = v[e] * g.alpha + bv[e];
             if (g.relu) x = fmaxf(x, 0.f);
-            if (g.drop_thresh) x *= tt_dropout_scale(g.drop_seed, gm, gn + e, g.drop_thresh, g.drop_inv_keep);
+            if (g.drop_thresh) x *= tt_dropout_scale(g.drop_seed, g.drop_row0 + (uint32_t)gm, gn + e, g.drop_thresh, g.drop_inv_keep);
             v[e] = x;
           }
           TO* dst = C + (long)gm * g.ldc + gn;
-          if (g.dbg & 1) {
-          } else if (gn + 8 <= g.N && g.vec_ok) {
+          if (gn + 8 <= g.N && g.vec_ok) {
             if (g.stream_out)
               st8_sc1(crs, (int)(((long)(gm - m0) * g.ldc + (gn - n0)) * (long)sizeof(TO)), v, (TO*)nullptr);
             else
@@ -464,8 +513,7 @@ int launch_gemm(int akout, int bkout, bool shift, GemmArgs& g, int nbatch, hipSt
   // persistent tiles with the epilogue under the next tile's first K-tiles: many tiles,
   // short K (the epilogue is a large share of a tile: measured faster up to 16 K-tiles,
   // slower at 48 and 128), no split-K, no accumulate (env TT_GEMM_PERSIST=0 disables)
-  static const char* pe = getenv("TT_GEMM_PERSIST");
-  const bool persist_ok = !(pe && pe[0] == '0');
+  const bool persist_ok = tt::opt(tt::OPT_GEMM_PERSIST) != 0;
   const int nk = (g.K * (int)sizeof(T) + ttg::KTB - 1) / ttg::KTB;
   if (dma && persist_ok && g.force_regstage == 0 && g.splits == 1 && !g.beta && nk >= 2 && nk <= 24 && t256 >= 512 &&
       use_big(g.M, g.N, t256))
@@ -544,9 +592,9 @@ extern "C" int tt_gemm(int dtype, int out_dtype, int a_kouter, int b_kouter, int
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = m; g.N = n; g.K = k;
   g.alpha = alpha; g.beta = beta_accum; g.relu = relu; g.seq_t = seq_t;
-  static const int force_reg = getenv("TT_GEMM_REGSTAGE") ? atoi(getenv("TT_GEMM_REGSTAGE")) : 0;
-  g.force_regstage = force_reg;
+  g.force_regstage = tt::opt(tt::OPT_GEMM_REGSTAGE);
   g.drop_seed = drop_seed;
+  g.drop_row0 = batch->drop_row0;
   g.drop_thresh = drop_p > 0.f ? (uint32_t)(drop_p * 16777216.0f + 0.5f) : 0u;
   g.drop_inv_keep = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
   const int nk = tt_ceil_div((long)k * esz, 128);
@@ -565,8 +613,7 @@ extern "C" int tt_gemm(int dtype, int out_dtype, int a_kouter, int b_kouter, int
     // outputs far larger than the L2s are streamed past them (sc1); ld*rows must
     // stay addressable by a 32-bit per-tile byte offset
     g.stream_out = ok && (long)m * n * osz >= (64L << 20) && (long)256 * ldc * osz < (1L << 31);
-    if (const char* e = getenv("TT_GEMM_STREAM_OUT")) g.stream_out = g.stream_out && atoi(e) != 0;
-    if (const char* e = getenv("TT_GEMM_DBG")) g.dbg = atoi(e);
+    g.stream_out = g.stream_out && tt::opt(tt::OPT_GEMM_STREAM_OUT) != 0;
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
   TT_CHECK_ARG((long)tt_ceil_div(m, 128) * tt_ceil_div(n, 128) * nbatch * splits < (1L << 31), "tt_gemm: too many tiles");

@@ -20,6 +20,7 @@ namespace {
 struct FwdRec {
   const void* g; const void* whh; const float* bhn; void* y; void* x1; void* save; float* hs;
   int dir; uint32_t seed; int col0;
+  uint32_t row0;  // dropout row of local row 0 (data-parallel: rank * B * T)
 };
 struct FwdArgs {
   FwdRec r[4];
@@ -28,8 +29,10 @@ struct FwdArgs {
   int s;
   uint32_t drop_thresh;
   float inv_keep;
-  int dbg;  // diagnostics (env TT_GRU_DBG): 1 no stores, 2 no G loads, 4 no MFMA, 8 no Whh stream
-  int stagger;  // persistent forward (compile-time NKT only): env TT_GRU_STAGGER
+  int stagger;  // persistent forward (compile-time NKT only): option gru_stagger
+#ifdef TT_DIAG
+  int dbg;  // diagnostic build only: 1 no stores, 2 no G loads
+#endif
 };
 
 struct BwdRec {
@@ -41,7 +44,9 @@ struct BwdArgs {
   int B, T, H;
   long ldy, ldd, ldf;
   int s;
-  int dbg;  // timing diagnostics only (env TT_GRU_DBG): 32 skips the GEMM, 64 the epilogue
+#ifdef TT_DIAG
+  int dbg;  // diagnostic build only: 1 no GEMM, 2 no epilogue loads, 4 no stores
+#endif
 };
 
 // B-tile row r of the forward step -> row (gate*H + j) of Whh [3H, H].
@@ -156,7 +161,7 @@ __global__ __launch_bounds__(256) void gru_fwd_step(FwdArgs a) {
         if (X1) {
 #pragma unroll
           for (int e = 0; e < 8; ++e)
-            y[e] *= a.drop_thresh ? tt_dropout_scale(R.seed, (uint32_t)row, (uint32_t)(R.col0 + j + e),
+            y[e] *= a.drop_thresh ? tt_dropout_scale(R.seed, R.row0 + (uint32_t)row, (uint32_t)(R.col0 + j + e),
                                                      a.drop_thresh, a.inv_keep)
                                   : 1.f;
           st8_sc1(xrs, (int)((((long)(b - m0) * T_) * a.ldy + j) * (long)sizeof(T)), y, (T*)nullptr);
@@ -191,7 +196,7 @@ __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
   for (int i = 0; i < ML::TM; ++i)
 #pragma unroll
     for (int j = 0; j < ML::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (!last && !(a.dbg & 32)) {
+  if (!last) {
     // dL/dgh_{s+1} = [dL/dar, dL/daz | dL/d(W_hn h)]: r|z from the dgx buffer, n from dgh
     ttg::KCSplit<T> la{DGX + (long)tn * a.ldd, DGH + (long)tn * a.ldd, (long)T_ * a.ldd, m0, a.B, 2 * H};
     ttg::KOPlain<T> lb{static_cast<const T*>(R.whh), H, j0, H - j0};
@@ -200,10 +205,6 @@ __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
     ML::run(la, lb, K, 0, nk, lds, acc);
   }
 
-  if (a.dbg & 64) {
-    if (threadIdx.x == 0 && acc[0][0][0] == 12345.f) R.dbias[0] = 1.f;  // keep the GEMM live
-    return;
-  }
   // ---- epilogue, one 64-row half at a time through LDS; each thread owns 8
   // consecutive units of a row (16-byte accesses) for 4 rows per half.
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, tid = threadIdx.x;
@@ -642,7 +643,11 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
   const __amdgpu_buffer_rsrc_t rY = tt_rsrc_n(Yw + r0w * a.ldy, true);
   const __amdgpu_buffer_rsrc_t rX1 = tt_rsrc_n(X1 ? X1 + r0w * a.ldy : Yw, X1 != nullptr);
   const __amdgpu_buffer_rsrc_t rS = tt_rsrc_n(S + r0w * 4L * H, true);
+#ifdef TT_DIAG
   const bool gok = rowok && !(a.dbg & 2), sok = rowok && !(a.dbg & 1);
+#else
+  const bool gok = rowok, sok = rowok;
+#endif
   // experimental: every step's block order starts at boff so the workgroups of one XCD
   // (blockIdx.x = x mod 8) stream different W_hh blocks at the same instant; hreg[i]
   // then holds block (boff + i) mod nblk. Compiled only into the fixed-NKT instances.
@@ -762,7 +767,8 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
           if (X1 && a.drop_thresh) {
 #pragma unroll
             for (int e = 0; e < 8; ++e)
-              y[e] *= tt_dropout_scale(R.seed, (uint32_t)row, (uint32_t)(R.col0 + j + e), a.drop_thresh, a.inv_keep);
+              y[e] *= tt_dropout_scale(R.seed, R.row0 + (uint32_t)row, (uint32_t)(R.col0 + j + e), a.drop_thresh,
+                                       a.inv_keep);
           }
           st16_buf(rX1, oy, 0, pack8bf(y));
         }
@@ -820,18 +826,14 @@ namespace {
 #endif
 bool gru_fwd_persistent(int dtype, int H) {
   if (dtype != TT_DT_BF16 || H % 64 != 0 || H > PH_MAX) return false;
-  const char* e = getenv("TT_GRU_STEP");
-  return !(e && e[0] == '1');
+  return tt::opt(tt::OPT_GRU_STEP) != 1;
 }
 
 }  // namespace
 
-// batch rows per backward tile: 128, or 64 with env TT_GRU_BWD_ROWS=64 (3 workgroups
+// batch rows per backward tile: 128, or 64 with option gru_bwd_rows = 64 (3 workgroups
 // per CU; measured slower at B=8192, H=512: 13.6 vs 11.5 ms per layer)
-static int bwd_rows() {
-  const char* e = getenv("TT_GRU_BWD_ROWS");
-  return (e && atoi(e) == 64) ? 64 : 128;
-}
+static int bwd_rows() { return tt::opt(tt::OPT_GRU_BWD_ROWS) == 64 ? 64 : 128; }
 extern "C" int tt_gru_bias_rows(int B) { return tt_ceil_div(B, bwd_rows()); }
 
 extern "C" int tt_gru_fwd_launches(int dtype, int T, int H) { return gru_fwd_persistent(dtype, H) ? 1 : T; }
@@ -871,18 +873,20 @@ extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B
   for (int i = 0; i < nrec; ++i) {
     const tt_gru_fwd_rec& r = recs[i];
     TT_CHECK_ARG(r.g && r.whh && r.bhn && r.y && r.save && r.hstate, "tt_gru_fwd: null pointer in rec %d", i);
-    a.r[i] = FwdRec{r.g, r.whh, r.bhn, r.y, r.x1, r.save, r.hstate, r.dir, r.drop_seed, r.drop_col0};
+    a.r[i] = FwdRec{r.g, r.whh, r.bhn, r.y, r.x1, r.save, r.hstate, r.dir, r.drop_seed, r.drop_col0, r.drop_row0};
   }
   a.B = B; a.T = T; a.H = H; a.ldg = ldg; a.ldy = ldy;
   a.drop_thresh = drop_p > 0.f ? (uint32_t)(drop_p * 16777216.0f + 0.5f) : 0u;
   a.inv_keep = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
+  a.stagger = tt::opt(tt::OPT_GRU_STAGGER);
+#ifdef TT_DIAG
   if (const char* e = getenv("TT_GRU_DBG")) a.dbg = atoi(e);
-  if (const char* e = getenv("TT_GRU_STAGGER")) a.stagger = atoi(e);
+#endif
   hipStream_t st = (hipStream_t)stream;
   if (gru_fwd_persistent(dtype, H)) {
     const dim3 grid(tt_ceil_div(B, PR) * nrec);
     int depth = (H / 64) % 4 == 0 ? 4 : (H / 64) % 2 == 0 ? 2 : 1;
-    if (const char* e = getenv("TT_GRU_DEPTH")) depth = std::min(depth, atoi(e));
+    depth = std::min(depth, tt::opt(tt::OPT_GRU_DEPTH));
     if (depth >= 4 && H == 512) hipLaunchKernelGGL((gru_fwd_seq<4, 8>), grid, dim3(PNT), 0, st, a);
     else if (depth >= 4 && H == 256) hipLaunchKernelGGL((gru_fwd_seq<4, 4>), grid, dim3(PNT), 0, st, a);
     else if (depth >= 4) hipLaunchKernelGGL((gru_fwd_seq<4, 0>), grid, dim3(PNT), 0, st, a);
@@ -919,12 +923,13 @@ extern "C" int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B
     TT_CHECK_HIP(hipMemsetAsync(r.dbias_part, 0, sizeof(float) * 4L * H * tt_gru_bias_rows(B), st));
   }
   a.B = B; a.T = T; a.H = H; a.ldy = ldy; a.ldd = ldd; a.ldf = ldf;
+#ifdef TT_DIAG
   if (const char* e = getenv("TT_GRU_DBG")) a.dbg = atoi(e);
+#endif
   const int bmr = bwd_rows();
   // bf16 with H a multiple of 256: 256x256 tiles on the 8-phase loop, one launch per step
-  // (env TT_GRU_BWD_BIG=0 selects the 128x128 step kernels)
-  const char* e5 = getenv("TT_GRU_BWD_BIG");
-  if (dtype == TT_DT_BF16 && H % 256 == 0 && bmr == 128 && !(e5 && e5[0] == '0')) {
+  // (option gru_bwd_big = 0 selects the 128x128 step kernels)
+  if (dtype == TT_DT_BF16 && H % 256 == 0 && bmr == 128 && tt::opt(tt::OPT_GRU_BWD_BIG) != 0) {
     const dim3 grid((H / 256) * tt_ceil_div(B, 256) * nrec);
     for (int s = T - 1; s >= 0; --s) {
       a.s = s;
@@ -936,8 +941,7 @@ extern "C" int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B
   // Two independent chains of step launches (recurrences [0, nrec/2) on the caller's
   // stream, the rest on a side stream): each step kernel is GEMM-then-epilogue, so one
   // chain's HBM-bound epilogues overlap the other chain's MFMA main loops on the same CUs.
-  const char* e2 = getenv("TT_GRU_BWD_STREAMS");
-  const int ngrp = (nrec >= 2 && !(e2 && atoi(e2) == 1)) ? 2 : 1;
+  const int ngrp = (nrec >= 2 && tt::opt(tt::OPT_GRU_BWD_STREAMS) != 1) ? 2 : 1;
   BwdArgs ga[2] = {a, a};
   int gn[2] = {nrec, 0};
   if (ngrp == 2) {

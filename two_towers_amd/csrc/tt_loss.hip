@@ -171,13 +171,16 @@ __global__ __launch_bounds__(256) void infonce_finalize_kernel(const float* __re
   row_loss[row] = v - diag[row];
 }
 
-// dS[i][j] = gscale * (softmax_ij - [j == label_i]) in dtype, full tiles.
+// dS[i][j] = g * (softmax_ij - [j == label_i]) in dtype, full tiles; g = *gscale (the
+// upstream gradient, read on the device: no host sync) or 1 when gscale is null.
 template <typename T>
 __global__ __launch_bounds__(256) void infonce_dscore_kernel(const T* __restrict__ qn, long bq,
                                                              const T* __restrict__ dn, long nd, int h, float inv_tau,
                                                              float offdiag, long label_off,
-                                                             const float* __restrict__ lse, float gscale,
-                                                             long ldds, T* __restrict__ ds) {
+                                                             const float* __restrict__ lse,
+                                                             const float* __restrict__ gscale, long ldds,
+                                                             T* __restrict__ ds) {
+  const float gs = gscale ? *gscale : 1.f;
   using ML = ttg::MainLoop<T, false, false, 128, 128>;
   __shared__ __attribute__((aligned(16))) char lds[ML::LDS_BYTES];
   const int m0 = blockIdx.y * 128, n0 = blockIdx.x * 128;
@@ -195,7 +198,7 @@ __global__ __launch_bounds__(256) void infonce_dscore_kernel(const T* __restrict
     float s = v * inv_tau;
     if (!lab) s -= offdiag;
     const float p = __expf(s - lse[row]);
-    Elt<T>::st(ds + row * ldds + col, gscale * (p - (lab ? 1.f : 0.f)));
+    Elt<T>::st(ds + row * ldds + col, gs * (p - (lab ? 1.f : 0.f)));
   });
 }
 
@@ -225,8 +228,9 @@ __global__ __launch_bounds__(256) void margin_fwd_kernel(const float* __restrict
 __global__ __launch_bounds__(256) void margin_bwd_kernel(const float* __restrict__ qn, long bq,
                                                          const float* __restrict__ dn, int h, long label_off,
                                                          const int32_t* __restrict__ idx, int k, float margin,
-                                                         float gscale, float* __restrict__ dqn,
+                                                         const float* __restrict__ gscale, float* __restrict__ dqn,
                                                          float* __restrict__ ddn) {
+  const float gs = gscale ? *gscale : 1.f;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= bq) return;
@@ -243,8 +247,8 @@ __global__ __launch_bounds__(256) void margin_bwd_kernel(const float* __restrict
   neg = wave_sum(neg) / k;
   // torch.clamp(min=0) passes the gradient where the argument is >= 0
   const bool active = (margin - pos + neg) >= 0.f;
-  const float gn = active ? gscale / k : 0.f;
-  const float gp = active ? -gscale : 0.f;
+  const float gn = active ? gs / k : 0.f;
+  const float gp = active ? -gs : 0.f;
   for (int c = lane; c < h; c += 64) {
     float d = gp * dp[c];
     for (int j = 0; j < k; ++j) d += gn * dn[(long)idx[row * k + j] * h + c];
@@ -273,8 +277,9 @@ constexpr int MB_ROWS = 64, MB_ENT = 2048, MB_HMAX = 512;
 __global__ __launch_bounds__(256) void margin_rows_kernel(const float* __restrict__ qn, long bq,
                                                           const float* __restrict__ dn, int h, long label_off,
                                                           const int32_t* __restrict__ idx, int k, float margin,
-                                                          float gscale, float* __restrict__ dqn,
+                                                          const float* __restrict__ gscale, float* __restrict__ dqn,
                                                           float2* __restrict__ coef) {
+  const float gs = gscale ? *gscale : 1.f;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= bq) return;
@@ -290,8 +295,8 @@ __global__ __launch_bounds__(256) void margin_rows_kernel(const float* __restric
   neg = wave_sum(neg) / k;
   // torch.clamp(min=0) passes the gradient where the argument is >= 0
   const bool active = (margin - pos + neg) >= 0.f;
-  const float gn = active ? gscale / k : 0.f;
-  const float gp = active ? -gscale : 0.f;
+  const float gn = active ? gs / k : 0.f;
+  const float gp = active ? -gs : 0.f;
   for (int c = lane; c < h; c += 64) {
     float d = gp * dp[c];
     for (int j = 0; j < k; ++j) d += gn * dn[(long)idx[row * k + j] * h + c];
@@ -456,7 +461,7 @@ extern "C" long tt_infonce_bwd_ws_size(int dtype, long bq, long nd, int h) {
 }
 
 extern "C" int tt_infonce_bwd(int dtype, const void* qn, long bq, const void* dn, long nd, int h, float inv_tau,
-                              float offdiag_sub, long label_offset, const float* lse, float gscale, float* dqn,
+                              float offdiag_sub, long label_offset, const float* lse, const float* gscale, float* dqn,
                               float* ddn, void* ws, void* stream) {
   TT_CHECK_ARG(dtype == TT_DT_F32 || dtype == TT_DT_BF16, "tt_infonce_bwd: bad dtype");
   TT_CHECK_ARG(label_offset >= 0 && label_offset + bq <= nd, "tt_infonce_bwd: labels outside [0, nd)");
@@ -558,7 +563,7 @@ extern "C" int tt_margin_fwd(const float* qn, long bq, const float* dn, long nd,
 extern "C" long tt_margin_bwd_ws_size(long bq) { return bq > 0 ? bq * 8 : 8; }
 
 extern "C" int tt_margin_bwd(const float* qn, long bq, const float* dn, long nd, int h, long label_offset,
-                             const int32_t* idx, int k, float margin, float gscale, float* dqn, float* ddn,
+                             const int32_t* idx, int k, float margin, const float* gscale, float* dqn, float* ddn,
                              void* ws, void* stream) {
   TT_CHECK_ARG(label_offset >= 0 && label_offset + bq <= nd && k >= 1, "tt_margin_bwd: bad labels/k");
   if (bq == 0) return 0;

@@ -443,11 +443,10 @@ int hn_run(const bf16_t* qn, long bq, const bf16_t* dn, long nd, long label_offs
 // Used by tt_hardneg_topk (tt_loss.hip) for bf16 operands with h in {128, 256}.
 long tt_hn_scan_ws_size(long bq, long nd, int k) { return hn_plan(bq, nd, k).bytes; }
 
-// TT_HN_GEMM=1 forces the GEMM + split top-k path (tests compare the two bit-exactly: both
-// produce every score with the same MFMA instruction and k order).
+// option hn_gemm = 1 forces the GEMM + split top-k path (tests compare the two bit-exactly:
+// both produce every score with the same MFMA instruction and k order).
 bool tt_hn_scan_supported(int dtype, int h) {
-  const char* env = getenv("TT_HN_GEMM");
-  const bool force_gemm = env != nullptr && env[0] == '1';
+  const bool force_gemm = tt::opt(tt::OPT_HN_GEMM) == 1;
   return !force_gemm && dtype == TT_BF16 && (h == 128 || h == 256);
 }
 

@@ -73,13 +73,14 @@ class _NormCE(torch.autograd.Function):
         inv_tau, offdiag, eps, do_norm, dt, group, rank, B = ctx.cfg
         h = qn.shape[1]
         nd = dn.shape[0]
-        gscale = float(gout)  # scalar upstream gradient (one D2H read per step)
+        # the scalar upstream gradient stays on the device: the kernels read it
+        gdev = gout.detach().float().reshape(1).contiguous()
         dqn = torch.empty(B, h, dtype=torch.float32, device=qn.device)
         ddn = torch.empty(nd, h, dtype=torch.float32, device=qn.device)
         lib = _lib.load()
         ws = torch.empty(lib.tt_infonce_bwd_ws_size(dtype_code(dt), B, nd, h), dtype=torch.uint8, device=qn.device)
         call("tt_infonce_bwd", dtype_code(dt), qn.data_ptr(), B, dn.data_ptr(), nd, h, inv_tau, offdiag, rank * B,
-             lse.data_ptr(), gscale, dqn.data_ptr(), ddn.data_ptr(), ws.data_ptr(), stream_ptr(qn.device))
+             lse.data_ptr(), gdev.data_ptr(), dqn.data_ptr(), ddn.data_ptr(), ws.data_ptr(), stream_ptr(qn.device))
         ddn_l = dist.reduce_scatter_rows(ddn, group)
         if do_norm:
             dq = ops.l2norm_bwd(dqn, qn32, qnorm, eps)
@@ -134,8 +135,10 @@ class _MarginFn(torch.autograd.Function):
         dqn = torch.empty_like(qn)
         ddn = torch.zeros_like(dn)
         ws = torch.empty(_lib.load().tt_margin_bwd_ws_size(B), dtype=torch.uint8, device=qn.device)
+        gdev = gout.detach().float().reshape(1).contiguous()  # read by the kernels: no host sync
         call("tt_margin_bwd", qn.data_ptr(), B, dn.data_ptr(), dn.shape[0], h, label_offset, idx.data_ptr(),
-             idx.shape[1], margin, float(gout), dqn.data_ptr(), ddn.data_ptr(), ws.data_ptr(), stream_ptr(qn.device))
+             idx.shape[1], margin, gdev.data_ptr(), dqn.data_ptr(), ddn.data_ptr(), ws.data_ptr(),
+             stream_ptr(qn.device))
         return ops.l2norm_bwd(dqn, qn, qnorm, eps), ops.l2norm_bwd(ddn, dn, dnorm, eps), None, None, None, None
 
 

@@ -31,7 +31,7 @@ import torch
 import torch.nn as nn
 from torch.utils.data import Dataset
 
-from . import _lib, ops, timing
+from . import _lib, dist, ops, timing
 from ._lib import Head1BwdIO, Head1FwdIO, call, dtype_code, stream_ptr
 from .losses import InfoNCELoss
 from .model import _GRU_ORDER
@@ -60,6 +60,11 @@ class _SharedHeadFn(torch.autograd.Function):
         rstd = torch.empty(rows, dtype=torch.float32, device=dev)
         out = torch.empty(rows, C, dtype=torch.float32, device=dev)
         seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if drop_p > 0 else 0
+        # rows are [queries; docs] stacked locally, so no single row offset maps them onto
+        # the global batch: data-parallel ranks draw from rank-distinct seeds instead
+        rank = dist.rank_world(None)[0]
+        if rank:
+            seed = (seed ^ (0x9E3779B9 * rank)) & 0x7FFFFFFF
         io = Head1FwdIO()
         io.x, io.w1, io.b1, io.ln_g, io.ln_b = x.data_ptr(), w.data_ptr(), b.data_ptr(), g.data_ptr(), be.data_ptr()
         io.p1, io.mean, io.rstd, io.out = p1.data_ptr(), mean.data_ptr(), rstd.data_ptr(), out.data_ptr()
@@ -182,7 +187,7 @@ class TwoTowerModel(nn.Module):
         if len(drops) != 1 or xs[0].shape[:2] != xs[-1].shape[:2] or xs[0].dtype != xs[-1].dtype:
             return tuple(self._towers([w], [x])[0] for w, x in zip(which, xs))
         cfg = TowerCfg(len(which), self.embedding_dim, self.hidden_dim, self.hidden_dim, self.compute_dtype,
-                       drops.pop(), head="none")
+                       drops.pop(), head="none", rank=dist.rank_world(getattr(self, "process_group", None))[0])
         params = []
         for e in encs:
             params.extend(getattr(e, n) for n in _GRU_ORDER)

@@ -16,7 +16,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import dist, ops
 from .towers import TowerCfg, run_towers
 
 
@@ -34,6 +34,7 @@ class EnhancedTwoTowerModel(nn.Module):
         self.embedding_dim = embedding_dim
         self.hidden_dim = hidden_dim
         self.compute_dtype = torch.float32
+        self.process_group = None  # data-parallel group (None: the default group when initialised)
         self._table = None  # not a parameter/buffer: keeps state_dict identical to the reference
 
     # ---------------------------------------------------------------- options
@@ -41,6 +42,13 @@ class EnhancedTwoTowerModel(nn.Module):
         if dtype not in (torch.float32, torch.bfloat16):
             raise ValueError("compute dtype must be torch.float32 or torch.bfloat16")
         self.compute_dtype = dtype
+        return self
+
+    def set_process_group(self, group):
+        """Data-parallel group the batch is split over. Only the dropout masks depend on it:
+        rank r's rows draw the masks of global rows r*B .. r*B+B-1, as one process running
+        the whole global batch would (so the ranks never repeat each other's masks)."""
+        self.process_group = group
         return self
 
     def set_embedding_table(self, table: torch.Tensor | None):
@@ -84,7 +92,7 @@ class EnhancedTwoTowerModel(nn.Module):
         if len(drops) != 1:
             return None
         return TowerCfg(ntowers, self.embedding_dim, 2 * self.hidden_dim, self.hidden_dim, self.compute_dtype,
-                        drops.pop())
+                        drops.pop(), rank=dist.rank_world(self.process_group)[0])
 
     def _run(self, which, xs):
         encs = [self.query_encoder if w == "query" else self.doc_encoder for w in which]

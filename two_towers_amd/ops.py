@@ -28,7 +28,7 @@ def gemm(a: Sequence[torch.Tensor], b: Sequence[torch.Tensor], c: Sequence[torch
          k: int, lda: int, ldb: int, ldc: int, a_kouter: bool, b_kouter: bool, dtype: torch.dtype,
          out_dtype: torch.dtype, bias: Sequence[torch.Tensor | None] | None = None,
          bshift: Sequence[int] | None = None, alpha: float = 1.0, accumulate: bool = False,
-         relu: bool = False, seq_t: int = 0, drop_seed: int = 0, drop_p: float = 0.0,
+         relu: bool = False, seq_t: int = 0, drop_seed: int = 0, drop_p: float = 0.0, drop_row0: int = 0,
          splits: int | None = None, a_hi: Sequence[torch.Tensor] | None = None, a_split: int = 0):
     """Batched C_i = alpha * op(A_i) op(B_i)^T (+bias) for up to 4 problems of one shape.
     With a_kouter and a_split > 0, A columns >= a_split are read from a_hi[i]."""
@@ -46,6 +46,7 @@ def gemm(a: Sequence[torch.Tensor], b: Sequence[torch.Tensor], c: Sequence[torch
         if a_split:
             bt.a_hi[i] = a_hi[i].data_ptr()
     bt.a_split = a_split
+    bt.drop_row0 = drop_row0 & 0xFFFFFFFF
     lib = _lib.load()
     if splits is None:
         splits = lib.tt_gemm_pick_splits(m, n, k, nb)

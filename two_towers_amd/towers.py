@@ -53,6 +53,7 @@ class TowerCfg:
     dtype: torch.dtype
     drop_p: float  # dropout between GRU layers (0 in eval)
     head: str = "proj2"  # "proj2": per-tower enhanced head; "none": return cat(h_fwd, h_rev) [B, 2H]
+    rank: int = 0  # data-parallel rank: dropout mask rows start at rank * B * T (global batch rows)
 
     @property
     def nparams(self) -> int:
@@ -128,6 +129,9 @@ def featurize(x: torch.Tensor, table: torch.Tensor | None, Ep: int, dt: torch.dt
 
 
 def _gru_layer_fwd(cfg, xs, K, ldx, packs, layer, B, T, seeds, want_x1):
+    """Input projection + one bidirectional GRU layer for every tower. The dropout copy
+    X1 (want_x1) draws keep(seed, rank*B*T + b*T + t, col): on N data-parallel ranks the
+    masks are those the single-process run of the global batch draws."""
     n, H, dt, dev = cfg.ntowers, cfg.H, cfg.dtype, xs[0].device
     BT = B * T
     G = [_alloc((BT, 6 * H), dt, dev) for _ in range(n)]
@@ -154,6 +158,7 @@ def _gru_layer_fwd(cfg, xs, K, ldx, packs, layer, B, T, seeds, want_x1):
             r.dir = d
             r.drop_seed = seeds[ti] & 0xFFFFFFFF
             r.drop_col0 = d * H
+            r.drop_row0 = (cfg.rank * B * T) & 0xFFFFFFFF
     # algorithmic bytes per (row, unit, step): gates 3 + h 1 + saved 4 (+ dropout copy 1)
     # elements of dt; the per-step kernel also re-reads h_{s-1} (1 element) and moves the
     # fp32 recurrent state through HBM (8 B), the persistent one keeps both on chip
@@ -351,7 +356,7 @@ class TowersFn(torch.autograd.Function):
                 for ti in range(n):
                     ops.gemm([dG1[ti]], [packs[ti].wih[1]], [dY0[ti]], m=B * T, n=2 * H, k=6 * H, lda=8 * H,
                              ldb=2 * H, ldc=2 * H, a_kouter=False, b_kouter=True, dtype=dt, out_dtype=dt,
-                             drop_seed=ctx.seeds[ti], drop_p=cfg.drop_p)
+                             drop_seed=ctx.seeds[ti], drop_p=cfg.drop_p, drop_row0=cfg.rank * B * T)
         del dG1
         # ---- GRU layer 0
         dG0, dbih0, dbhh0 = _gru_layer_bwd(cfg, 0, B, T, S0, Y0, dY0, None, packs)

@@ -145,7 +145,7 @@ def cpu_baseline(args):
 # MI355X_MICROARCH.md). A region launch may cover several dispatches (the GRU backward
 # runs two chains of step kernels), hence the dispatches-per-step scaling.
 PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_summary.json")
-REGION_KERNEL = {"gru_bwd_step": ("gru_bwd_step<", "gru_bwd_big"), "gru_fwd": ("gru_fwd_seq<",),
+REGION_KERNEL = {"gru_bwd_step": ("gru_bwd_step<", "gru_bwd_big", "gru_bwd_rows<"), "gru_fwd": ("gru_fwd_seq<",),
                  "embed_gather": ("embed_gather_kernel",)}
 
 

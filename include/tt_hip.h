@@ -41,7 +41,7 @@ const char* tt_last_error(void);
 /* Kernel-variant switches (process-wide; initialised once from the environment variable
  * of the same name in upper case with a TT_ prefix, e.g. gru_step <- TT_GRU_STEP):
  * gru_step, gru_depth, gru_stagger, gru_bwd_rows, gru_bwd_big, gru_bwd_streams,
- * gemm_persist, gemm_regstage, gemm_stream_out, hn_gemm. Every variant computes the
+ * gemm_persist, gemm_regstage, gemm_stream_out, hn_gemm, gru_bwd_persist. Every variant computes the
  * same function; they exist for A/B measurement and for tests that compare variants.
  * Not synchronised with launches in flight: set them between steps. */
 int tt_set_option(const char* name, int value);
@@ -154,6 +154,9 @@ typedef struct {
 
 int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B, int T, int H, long ldy,
                long ldd, long ldf, void* stream);
+/* Kernel launches tt_gru_bwd issues: 1 for the row-owning bf16 kernel (H 256 or 512: one
+ * workgroup per 128 batch rows x all H units walks every step), T otherwise. */
+int tt_gru_bwd_launches(int dtype, int T, int H);
 int tt_gru_bias_rows(int B);
 
 /* ------------------------------------------------------------ projection head */

@@ -219,3 +219,29 @@ def test_big_tile_gru_backward_matches_step_kernel(B, T):
         a, b = outs[1][k].double(), outs[0][k].double()
         cos = float((a * b).sum() / (a.norm() * b.norm() + 1e-30))
         assert cos > 0.9999 and rel(outs[1][k], outs[0][k]) < 2e-2, (k, cos)
+
+
+@pytest.mark.parametrize("h,B,T", [(256, 130, 5), (256, 520, 3), (128, 200, 6)])
+def test_row_owning_gru_backward_matches_step_kernels(h, B, T):
+    """bf16 backward through the persistent row-owning kernel (gru_bwd_rows: one launch
+    per layer, 128 rows x all H units per workgroup, H 512 / 256) vs the per-step launches
+    (option gru_bwd_persist = 0): the same arithmetic per element, so gradients agree to
+    accumulation order (the recurrent GEMM's K order and the bias partial sums differ).
+    B 130 / 520 / 200 give tail row tiles."""
+    E = 40
+    g = torch.Generator().manual_seed(13)
+    q = torch.randn(B, T, E, generator=g).to(DEV)
+    d = torch.randn(B, T, E, generator=g).to(DEV)
+    outs = []
+    for persist in (0, 1):
+        m, _ = make_model(E, h, 5)
+        m = m.to(DEV).train().set_compute_dtype(torch.bfloat16)
+        with option("gru_bwd_persist", persist):
+            qv, dv = m(q, d)
+            loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
+            loss.backward()
+        outs.append({k: p.grad.clone() for k, p in m.named_parameters()})
+    for k in outs[0]:
+        a, b = outs[1][k].double(), outs[0][k].double()
+        cos = float((a * b).sum() / (a.norm() * b.norm() + 1e-30))
+        assert cos > 0.9999 and rel(outs[1][k], outs[0][k]) < 2e-2, (k, cos)

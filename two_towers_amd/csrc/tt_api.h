@@ -23,6 +23,7 @@ enum Opt {
   OPT_GEMM_REGSTAGE,    // 1/2: force register staging / 128-tiles (9: no epilogue, timing)
   OPT_GEMM_STREAM_OUT,  // 0: no write-through output stores
   OPT_HN_GEMM,          // 1: hard-negative top-k through GEMM + split top-k, no scan
+  OPT_GRU_BWD_PERSIST,  // 0: per-step backward launches instead of the row-owning kernel
   OPT_N
 };
 int opt(Opt o);

@@ -511,6 +511,228 @@ __global__ __launch_bounds__(512) void gru_bwd_big(BwdArgs a) {
   }
 }
 
+// ---- persistent ("row-owning") backward, bf16, H in {256, 512} --------------------
+// One launch per layer. A workgroup (8 waves) owns 128 batch rows x ALL H units of one
+// recurrence and walks every time step itself: batch rows never interact, so no step
+// waits for another workgroup, and workgroups drift out of phase -- one CU's HBM-bound
+// epilogue streams while another's recurrent GEMM runs, instead of every CU doing the
+// GEMM (HBM idle) and then the epilogue (MFMA idle) in lockstep, once per launch.
+// Per step: acc[128 x H] = dL/dgh_{s+1}[128 x 3H] . W_hh[3H x H] on MFMA (A: the rows'
+// own gradients of the previous iteration, K-contig, r|z from dgx and n from dgh; B: W_hh,
+// K-outer, read from the XCD's L2), then the gate gradients in two 64-row passes staged
+// through the freed LDS; the step's bias partials are added into the tile's partial row.
+//   LDS: 2 slots x (A 16 KiB + H/128 B sub-images of 16 KiB) = 160 KiB at H = 512.
+// Waves as 2 (rows) x 4 (columns): wave tile 64 x H/4, acc[4][H/64] of 16x16 MFMA tiles.
+template <int H>
+struct BwdRowsCfg {
+  static constexpr int NQ = H / 128;             // B sub-images per K-tile
+  static constexpr int SLOT = (1 + NQ) * 16384;  // one K-tile: A + B
+  static constexpr int LDS = 2 * SLOT;
+  static constexpr int NCB = H / 64;             // 16-column blocks per wave
+  static constexpr int TPR = H / 8;              // epilogue threads per row (8 units each)
+  static constexpr int RPI = 512 / TPR;          // rows per epilogue iteration
+  static constexpr int LDF = H + 16;             // staged fp32 row stride (bank spread)
+  static_assert(64 * LDF * 4 <= LDS && RPI * 4 * H * 4 <= LDS, "staging fits the slots");
+};
+
+template <int H>
+__global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
+  using C = BwdRowsCfg<H>;
+  using L8 = ttg::Loop8<bf16_t, false, true>;
+  __shared__ __attribute__((aligned(16))) char lds[C::LDS];
+  const int T_ = a.T, ntm = (a.B + 127) / 128;
+  const int id = ttg::xcd_remap(blockIdx.x, gridDim.x);
+  const int rz = id / ntm, mt = id - rz * ntm;
+  const BwdRec R = a.r[rz];
+  const int m0 = mt * 128;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave >> 2, wc = wave & 3;
+  const bf16_t* DGX = static_cast<const bf16_t*>(R.dgx);
+  const bf16_t* DGH = static_cast<const bf16_t*>(R.dgh);
+  bf16_t* DGXw = static_cast<bf16_t*>(R.dgx);
+  bf16_t* DGHw = static_cast<bf16_t*>(R.dgh);
+  const bf16_t* S = static_cast<const bf16_t*>(R.save);
+  const bf16_t* Y = static_cast<const bf16_t*>(R.y);
+  const bf16_t* DY = static_cast<const bf16_t*>(R.dy);
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane(ttg::lds_addr_of(lds));
+  constexpr int K = 3 * H, NK = K / L8::KTE;
+  const long dk = (long)L8::KTE * H * 2;  // bytes between K-tiles of the K-outer W_hh
+  const ttg::KOPlain<bf16_t> lb{static_cast<const bf16_t*>(R.whh), H, 0, H};
+  // epilogue ownership: units jg .. jg+7 of rows rsub + RPI i
+  const int jg = (tid % C::TPR) * 8, rsub = tid / C::TPR;
+  float* L = reinterpret_cast<float*>(lds);
+  float* part = R.dbias + (long)mt * (4L * H);  // this tile's partial row (zeroed by the host)
+
+  for (int s = T_ - 1; s >= 0; --s) {
+    const int t = R.dir ? T_ - 1 - s : s;
+    const int tn = R.dir ? t - 1 : t + 1;
+    const int tp = R.dir ? t + 1 : t - 1;
+    const bool last = (s == T_ - 1);
+    f32x4 acc[4][C::NCB];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < C::NCB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (!last) {
+      // A = dL/dgh_{s+1} of this workgroup's rows, written by its own previous iteration
+      const ttg::KCSplit<bf16_t> la{DGX + (long)tn * a.ldd, DGH + (long)tn * a.ldd, (long)T_ * a.ldd, m0, a.B, 2 * H};
+      typename L8::Piece pa[2], pb[C::NQ][2];
+      L8::template init_half<false>(la, 0, NK, K, 0, pa);
+#pragma unroll
+      for (int q = 0; q < C::NQ; ++q) L8::template init_half<true>(lb, 0, NK, K, 128 * q, pb[q]);
+      L8::issue_half(la, pa, 0, (long)ttg::KTB, lbase);
+#pragma unroll
+      for (int q = 0; q < C::NQ; ++q) L8::issue_half(lb, pb[q], 0, dk, lbase + 16384u * (1 + q));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      for (int r = 0; r < NK; ++r) {
+        const int cs = r & 1;
+        const char* sl = lds + cs * C::SLOT;
+        if (r + 1 < NK) {  // K-tile r+1 flies during K-tile r's MFMAs; its slot was freed by
+                           // the barrier that ended K-tile r-1
+          const uint32_t nx = lbase + (cs ^ 1) * C::SLOT;
+          L8::issue_half(la, pa, r + 1, (long)ttg::KTB, nx);
+#pragma unroll
+          for (int q = 0; q < C::NQ; ++q) L8::issue_half(lb, pb[q], r + 1, dk, nx + 16384u * (1 + q));
+        }
+        uint4 fa[2][4];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) fa[ks][i] = ttg::frag<bf16_t, false>(sl, wr * 64 + 16 * i, ks);
+        const char* ib = sl + 16384 + ((wc * (H / 4)) >> 7) * 16384;
+        const int cb = (wc * (H / 4)) & 127;
+#pragma unroll
+        for (int jp = 0; jp < C::NCB; jp += 2) {
+          uint4 fb[2][2];
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) fb[ks][j] = ttg::frag<bf16_t, true>(ib, cb + 16 * (jp + j), ks);
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int j = 0; j < 2; ++j) acc[i][jp + j] = ttg::mma<bf16_t>(fa[ks][i], fb[ks][j], acc[i][jp + j]);
+          __builtin_amdgcn_s_setprio(0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of K-tile r+1
+        __builtin_amdgcn_s_barrier();                      // everyone's; slot cs is free
+      }
+    }
+    // ---- epilogue in two passes over an fp32 [64][LDF] image in the freed slots: pass p
+    // stages accumulator rows 32p..32p+31 of BOTH wave rows (image row ri <-> tile row
+    // (ri / 32) * 64 + 32p + ri % 32), so half of every wave's accumulators die before the
+    // first pass's gate arithmetic (the register budget of the two-wave-per-SIMD kernel)
+    const long trow = (long)m0 * T_ + t;
+    // carry dh*z in bf16: an fp32 carry measured the same gradient error vs the fp32
+    // oracle (tools/diag_bench_path.py) at 10 % more time
+    const __amdgpu_buffer_rsrc_t rc =
+        tt_rsrc_n(static_cast<const bf16_t*>(R.dh) + (long)((s + 1) & 1) * a.B * H + (long)m0 * H, !last);
+    bf16_t* cr_cur = static_cast<bf16_t*>(R.dh) + (long)(s & 1) * a.B * H + (long)m0 * H;
+    const __amdgpu_buffer_rsrc_t rd = tt_rsrc_n(DY ? DY + trow * a.ldy : S, DY != nullptr);
+    const __amdgpu_buffer_rsrc_t rsv = tt_rsrc_n(S + trow * 4L * H, true);
+    const __amdgpu_buffer_rsrc_t ry = tt_rsrc_n(s > 0 ? Y + ((long)m0 * T_ + tp) * a.ldy : S, s > 0);
+    const __amdgpu_buffer_rsrc_t grs = tt_rsrc(DGXw + trow * a.ldd);
+    float bsum[4][8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bsum[q][e] = 0.f;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int jc = 0; jc < C::NCB; ++jc)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            L[(wr * 32 + 16 * ii + 4 * (lane >> 4) + e) * C::LDF + wc * (H / 4) + 16 * jc + (lane & 15)] =
+                acc[2 * p + ii][jc][e];
+      __syncthreads();
+      constexpr int NB = 1;  // rows per load batch (two do not fit the VGPR budget)
+#pragma unroll 1
+      for (int kb = 0; kb < 64 / C::RPI; kb += NB) {
+        uint4 vin[NB][7];
+#pragma unroll
+        for (int kk = 0; kk < NB; ++kk) {
+          const int ri = rsub + C::RPI * (kb + kk);
+          const int bl = (ri >> 5) * 64 + 32 * p + (ri & 31);  // row within the tile
+          const bool ok = m0 + bl < a.B;
+          const uint32_t oc = ok ? (uint32_t)(bl * H + jg) * 2u : 0x80000000u;
+          const uint32_t oy = ok ? (uint32_t)(bl * T_ * (int)a.ldy + jg) * 2u : 0x80000000u;
+          const uint32_t os = ok ? (uint32_t)(bl * T_ * 4 * H + jg) * 2u : 0x80000000u;
+          vin[kk][0] = ld16_buf(rc, oc, 0);
+          vin[kk][1] = ld16_buf(rd, oy, 0);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) vin[kk][2 + q] = ld16_buf(rsv, os, q * 2 * H);
+          vin[kk][6] = ld16_buf(ry, oy, 0);
+        }
+#pragma unroll
+        for (int kk = 0; kk < NB; ++kk) {
+          const int ri = rsub + C::RPI * (kb + kk);
+          const int bl = (ri >> 5) * 64 + 32 * p + (ri & 31);
+          const int b = m0 + bl;
+          if (b >= a.B) continue;
+          float cin[8], dy[8], ar[8], az[8], an[8], gh[8], hp[8];
+          unpack8(vin[kk][0], cin);
+          unpack8(vin[kk][1], dy);
+          unpack8(vin[kk][2], ar);
+          unpack8(vin[kk][3], az);
+          unpack8(vin[kk][4], an);
+          unpack8(vin[kk][5], gh);
+          unpack8(vin[kk][6], hp);
+          if (last && R.dfinal) ld8(R.dfinal + (long)b * a.ldf + jg, cin);  // fp32 final-state gradient
+          const float* Lc = L + ri * C::LDF + jg;
+          float o_r[8], o_z[8], o_n[8], o_hn[8], cout[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float dht = Lc[e] + cin[e] + dy[e];
+            float rg, omr, zg, omz, ng, sech2;
+            tt_sigmoid_pair(ar[e], rg, omr);
+            tt_sigmoid_pair(az[e], zg, omz);
+            tt_tanh_sech2(an[e], ng, sech2);
+            const float dnp = dht * omz * sech2;
+            const float drp = dnp * gh[e] * rg * omr;
+            const float dzp = dht * (hp[e] - ng) * zg * omz;
+            o_r[e] = drp; o_z[e] = dzp; o_n[e] = dnp; o_hn[e] = dnp * rg;
+            cout[e] = dht * zg;
+            bsum[0][e] += drp; bsum[1][e] += dzp; bsum[2][e] += dnp; bsum[3][e] += dnp * rg;
+          }
+          st8(cr_cur + (long)bl * H + jg, cout);
+          const long row = (long)b * T_ + t;
+          bf16_t* xw = DGXw + row * a.ldd + jg;
+          st8(xw, o_r);
+          st8(xw + H, o_z);
+          st8_sc1(grs, (int)(((long)bl * T_ * a.ldd + jg + 2 * H) * 2L), o_n, (bf16_t*)nullptr);
+          st8(DGHw + row * a.ldd + jg, o_hn);
+        }
+      }
+      __syncthreads();  // the image is rewritten by the next pass / the bias reduction
+    }
+    // the step's bias partials: the RPI threads sharing each unit group meet in LDS, then
+    // one add per column into the tile's partial row (owned by this workgroup alone)
+    float* red = L;  // [RPI][4][H]
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[(rsub * 4 + q) * H + jg + e] = bsum[q][e];
+    __syncthreads();
+    for (int c = tid; c < 4 * H; c += 512) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < C::RPI; ++w) v += red[w * 4 * H + c];
+      part[c] += v;
+    }
+    // this step's dL/dgh and carry are the next iteration's operands: every wave's stores
+    // must have reached L2 before any wave issues the DMA that reads them
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+}
+
 // ---- persistent ("row-resident") forward, bf16 ---------------------------------
 // Batch rows never interact, so one workgroup can own 64 rows of one recurrence for
 // all T steps: h_{s-1} stays in LDS as the A operand (bf16 KC image, never re-read
@@ -838,6 +1060,11 @@ extern "C" int tt_gru_bias_rows(int B) { return tt_ceil_div(B, bwd_rows()); }
 
 extern "C" int tt_gru_fwd_launches(int dtype, int T, int H) { return gru_fwd_persistent(dtype, H) ? 1 : T; }
 
+static bool gru_bwd_persistent(int dtype, int H) {
+  return dtype == TT_DT_BF16 && (H == 256 || H == 512) && bwd_rows() == 128 && tt::opt(tt::OPT_GRU_BWD_PERSIST) != 0;
+}
+extern "C" int tt_gru_bwd_launches(int dtype, int T, int H) { return gru_bwd_persistent(dtype, H) ? 1 : T; }
+
 // Per-device side stream + fork/join events for tt_gru_bwd's second launch chain.
 struct SideStream {
   hipStream_t s = nullptr;
@@ -927,6 +1154,16 @@ extern "C" int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B
   if (const char* e = getenv("TT_GRU_DBG")) a.dbg = atoi(e);
 #endif
   const int bmr = bwd_rows();
+  // bf16, H 256 / 512: one row-owning launch per layer (option gru_bwd_persist = 0: per-step
+  // launches)
+  if (gru_bwd_persistent(dtype, H)) {
+    TT_CHECK_ARG(128L * T * std::max({ldd, ldy, 4L * H}) * esz < (1L << 31), "tt_gru_bwd: tile offsets exceed 2 GiB");
+    const dim3 grid(tt_ceil_div(B, 128) * nrec);
+    if (H == 512) hipLaunchKernelGGL(gru_bwd_rows<512>, grid, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL(gru_bwd_rows<256>, grid, dim3(512), 0, st, a);
+    TT_CHECK_LAUNCH("gru_bwd_rows");
+    return 0;
+  }
   // bf16 with H a multiple of 256: 256x256 tiles on the 8-phase loop, one launch per step
   // (option gru_bwd_big = 0 selects the 128x128 step kernels)
   if (dtype == TT_DT_BF16 && H % 256 == 0 && bmr == 128 && tt::opt(tt::OPT_GRU_BWD_BIG) != 0) {

@@ -201,8 +201,9 @@ def _gru_layer_bwd(cfg, layer, B, T, S, Y, dY, dfinal, packs):
     # operand) + 4 written gradients (r, z, n, W_hn h) + the carry read and written, all
     # of dt
     esz = 2 if dt == torch.bfloat16 else 4
-    with timing.region("gru_bwd_step", T, 2.0 * B * 3 * H * H * 2 * n * (T - 1),
-                       float(B * T * H * 2 * n * esz * (14 + (1 if dY is not None else 0)))):
+    nl = lib.tt_gru_bwd_launches(dtype_code(dt), T, H)
+    per = esz * (14 + (1 if dY is not None else 0))
+    with timing.region("gru_bwd_step", nl, 2.0 * B * 3 * H * H * 2 * n * (T - 1), float(B * T * H * 2 * n * per)):
         call("tt_gru_bwd", dtype_code(dt), recs, 2 * n, B, T, H, 2 * H, 8 * H, ldf, stream_ptr(dev))
     sums = _alloc((n * 2, 4 * H), torch.float32, dev)
     for i in range(2 * n):

@@ -125,3 +125,38 @@ def test_hardneg_margin_bf16_b1024_agrees_with_fp32():
         a, b = a.double().cpu(), b.double()
         assert float((a - b).abs().max() / b.abs().max()) <= 1e-4
     print(f"hard negatives: {same.mean():.4f} of rows pick the fp32 set; loss {float(loss):.6f}")
+
+
+def test_reference_size_h512_bf16_matches_oracle():
+    """hidden_dim 512 (GRU H = 1024), the reference's own training size
+    (train_enhanced.py:30) and BASELINE configs[4]'s model, in bf16 at T = 32 (configs[4]
+    runs T = 128): the per-step bf16 forward (H > 512 exceeds the row-resident kernel's
+    LDS image) and the 256x256 BPTT step kernel (gru_bwd_big), against the fp32 oracle on
+    bf16-rounded operands, with the tolerances stated at the top of this file."""
+    Hd, Tq, Bq = 512, 32, 64
+    torch.manual_seed(35)
+    m = tta.EnhancedTwoTowerModel(E, Hd)
+    with torch.no_grad():
+        for prm in m.parameters():
+            prm.copy_(_bf16(prm))
+    p = {k: v.detach().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    m = m.to(DEV).set_compute_dtype(torch.bfloat16).train()
+    g = torch.Generator().manual_seed(36)
+    q = _bf16(torch.randn(Bq, Tq, E, generator=g) * 0.5)
+    d = _bf16(torch.randn(Bq, Tq, E, generator=g) * 0.5)
+    torch.manual_seed(37)
+    qv, dv = m(q.to(DEV), d.to(DEV))
+    loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
+    loss.backward()
+    torch.manual_seed(37)
+    seeds = [int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) for _ in range(2)]
+    rq, rd = cpu_ref.forward(q, d, p, drop_p=0.1, seeds=seeds)
+    rl = cpu_ref.infonce(rq, rd)
+    rl.backward()
+    lv, rv = float(loss.detach()), float(rl.detach())
+    assert abs(lv - rv) <= 2e-3 * abs(rv), (lv, rv)
+    for a, b in ((qv, rq), (dv, rd)):
+        a, b = a.detach().double().cpu(), b.detach().double()
+        assert float((a - b).abs().max() / b.abs().max()) <= 3e-2
+    frob, cos, k = _grad_check(dict(m.named_parameters()), p)
+    print(f"h 512: loss {lv:.6f} vs {rv:.6f}; worst gradient {k}: rel {frob:.4f}, cos {cos:.5f}")

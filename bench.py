@@ -144,7 +144,13 @@ def cpu_baseline(args):
 # hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1 KiB per dispatch, the gfx950 correction of
 # MI355X_MICROARCH.md). A region launch may cover several dispatches (the GRU backward
 # runs two chains of step kernels), hence the dispatches-per-step scaling.
-PMC_SUMMARY = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_summary.json")
+def _latest_pmc():
+    import glob
+    found = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*_pmc_summary.json")))
+    return found[-1] if found else ""
+
+
+PMC_SUMMARY = _latest_pmc()
 REGION_KERNEL = {"gru_bwd_step": ("gru_bwd_step<", "gru_bwd_big", "gru_bwd_rows<"), "gru_fwd": ("gru_fwd_seq<",),
                  "embed_gather": ("embed_gather_kernel",)}
 
@@ -161,7 +167,7 @@ def pmc_traffic(region, launches_per_step):
         return {"traffic": None}
     per_step = sum(v["hbm_bytes_est"] * v["dispatches_per_step"] for v in hits)
     return {"traffic": round(per_step / max(launches_per_step, 1)), "traffic_unit": "bytes/launch",
-            "traffic_source": "profiles/r01_pmc_summary.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE)"}
+            "traffic_source": f"profiles/{os.path.basename(PMC_SUMMARY)} (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE)"}
 
 
 def main():

@@ -79,11 +79,13 @@ def main():
     dev = torch.device("cuda")
     recs, keep = setup(a.B, a.T, a.H, dev)
     st = stream_ptr(dev)
+    call("tt_gru_fwd", 1, recs, 4, a.B, a.T, a.H, 6 * a.H, 2 * a.H, 0.1, st)  # real S / Y for the backward
     for v in a.bwd_variants.split(","):
         if not v:
             continue
         rows, dbg, strm = (v.split(":") + ["0", "2"])[:3]
-        set_option("gru_bwd_rows", int(rows))
+        set_option("gru_bwd_persist", 1 if rows == "P" else 0)
+        set_option("gru_bwd_rows", 128 if rows == "P" else int(rows))
         os.environ["TT_GRU_DBG"] = dbg  # read only by a -DTT_DIAG build
         set_option("gru_bwd_streams", int(strm))
         brecs, bkeep = setup_bwd(a.B, a.T, a.H, keep, dev)

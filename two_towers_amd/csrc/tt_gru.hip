@@ -519,9 +519,11 @@ __global__ __launch_bounds__(512) void gru_bwd_big(BwdArgs a) {
 // GEMM (HBM idle) and then the epilogue (MFMA idle) in lockstep, once per launch.
 // Per step: acc[128 x H] = dL/dgh_{s+1}[128 x 3H] . W_hh[3H x H] on MFMA (A: the rows'
 // own gradients of the previous iteration, K-contig, r|z from dgx and n from dgh; B: W_hh,
-// K-outer, read from the XCD's L2), then the gate gradients in two 64-row passes staged
-// through the freed LDS; the step's bias partials are added into the tile's partial row.
-//   LDS: 2 slots x (A 16 KiB + H/128 B sub-images of 16 KiB) = 160 KiB at H = 512.
+// K-outer, read from the XCD's L2), then the gate gradients with the accumulator tile
+// staged through the freed LDS; the step's bias partials are added into the tile's
+// partial row.
+//   LDS: 2 slots x (A 16 KiB + H/128 B sub-images of 16 KiB) = 160 KiB at H = 512; the
+//   epilogue's bf16 [128][H] accumulator image reuses them.
 // Waves as 2 (rows) x 4 (columns): wave tile 64 x H/4, acc[4][H/64] of 16x16 MFMA tiles.
 template <int H>
 struct BwdRowsCfg {
@@ -531,8 +533,8 @@ struct BwdRowsCfg {
   static constexpr int NCB = H / 64;             // 16-column blocks per wave
   static constexpr int TPR = H / 8;              // epilogue threads per row (8 units each)
   static constexpr int RPI = 512 / TPR;          // rows per epilogue iteration
-  static constexpr int LDF = H + 16;             // staged fp32 row stride (bank spread)
-  static_assert(64 * LDF * 4 <= LDS && RPI * 4 * H * 4 <= LDS, "staging fits the slots");
+  static constexpr int LDB = H + 8;              // staged bf16 row pitch (bank spread)
+  static_assert(128 * LDB * 2 <= LDS && RPI * 4 * H * 4 <= LDS, "staging fits the slots");
 };
 
 template <int H>
@@ -562,6 +564,11 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
   const int jg = (tid % C::TPR) * 8, rsub = tid / C::TPR;
   float* L = reinterpret_cast<float*>(lds);
   float* part = R.dbias + (long)mt * (4L * H);  // this tile's partial row (zeroed by the host)
+#ifdef TT_DIAG
+  const int dbg = a.dbg;  // diagnostic build only: 1 no GEMM, 2 no epilogue loads, 4 no stores
+#else
+  constexpr int dbg = 0;
+#endif
 
   for (int s = T_ - 1; s >= 0; --s) {
     const int t = R.dir ? T_ - 1 - s : s;
@@ -573,16 +580,24 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < C::NCB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (!last) {
+    if (!last && !(dbg & 1)) {
       // A = dL/dgh_{s+1} of this workgroup's rows, written by its own previous iteration
       const ttg::KCSplit<bf16_t> la{DGX + (long)tn * a.ldd, DGH + (long)tn * a.ldd, (long)T_ * a.ldd, m0, a.B, 2 * H};
-      typename L8::Piece pa[2], pb[C::NQ][2];
+      // B pieces: sub-image q is the same pattern 128 columns (256 B) further right, and
+      // W_hh is fully in range, so one piece per DMA slot serves all q
+      typename L8::Piece pa[2], pb[2];
       L8::template init_half<false>(la, 0, NK, K, 0, pa);
+      L8::template init_half<true>(lb, 0, NK, K, 0, pb);
+      auto issue_b = [&](int r, uint32_t img) {
+        const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
-      for (int q = 0; q < C::NQ; ++q) L8::template init_half<true>(lb, 0, NK, K, 128 * q, pb[q]);
+        for (int q = 0; q < C::NQ; ++q)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            ttg::dma16(pb[j].p + (long)r * dk + 256 * q, img + 16384u * (1 + q) + (uint32_t)(wv + 8 * j) * 1024u);
+      };
       L8::issue_half(la, pa, 0, (long)ttg::KTB, lbase);
-#pragma unroll
-      for (int q = 0; q < C::NQ; ++q) L8::issue_half(lb, pb[q], 0, dk, lbase + 16384u * (1 + q));
+      issue_b(0, lbase);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       for (int r = 0; r < NK; ++r) {
@@ -592,8 +607,7 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
                            // the barrier that ended K-tile r-1
           const uint32_t nx = lbase + (cs ^ 1) * C::SLOT;
           L8::issue_half(la, pa, r + 1, (long)ttg::KTB, nx);
-#pragma unroll
-          for (int q = 0; q < C::NQ; ++q) L8::issue_half(lb, pb[q], r + 1, dk, nx + 16384u * (1 + q));
+          issue_b(r + 1, nx);
         }
         uint4 fa[2][4];
 #pragma unroll
@@ -622,10 +636,10 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
         __builtin_amdgcn_s_barrier();                      // everyone's; slot cs is free
       }
     }
-    // ---- epilogue in two passes over an fp32 [64][LDF] image in the freed slots: pass p
-    // stages accumulator rows 32p..32p+31 of BOTH wave rows (image row ri <-> tile row
-    // (ri / 32) * 64 + 32p + ri % 32), so half of every wave's accumulators die before the
-    // first pass's gate arithmetic (the register budget of the two-wave-per-SIMD kernel)
+    // ---- epilogue: the whole 128 x H accumulator tile is staged at once as a bf16 image
+    // [128][LDB] over the freed slots (the recurrent term rounded to bf16 like the carry
+    // and the GEMM operands it is summed with), so every accumulator register is free
+    // before the gate arithmetic and the rows' loads can be batched NB deep.
     const long trow = (long)m0 * T_ + t;
     // carry dh*z in bf16: an fp32 carry measured the same gradient error vs the fp32
     // oracle (tools/diag_bench_path.py) at 10 % more time
@@ -636,82 +650,82 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
     const __amdgpu_buffer_rsrc_t rsv = tt_rsrc_n(S + trow * 4L * H, true);
     const __amdgpu_buffer_rsrc_t ry = tt_rsrc_n(s > 0 ? Y + ((long)m0 * T_ + tp) * a.ldy : S, s > 0);
     const __amdgpu_buffer_rsrc_t grs = tt_rsrc(DGXw + trow * a.ldd);
+    uint32_t* L16 = reinterpret_cast<uint32_t*>(lds);  // bf16 image, row pitch LDB elements
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jc = 0; jc < C::NCB; ++jc)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          reinterpret_cast<bf16_t*>(lds)[(wr * 64 + 16 * i + 4 * (lane >> 4) + e) * C::LDB + wc * (H / 4) + 16 * jc +
+                                         (lane & 15)] = f2bf(acc[i][jc][e]);
+    __syncthreads();
     float bsum[4][8];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int e = 0; e < 8; ++e) bsum[q][e] = 0.f;
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-        for (int jc = 0; jc < C::NCB; ++jc)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            L[(wr * 32 + 16 * ii + 4 * (lane >> 4) + e) * C::LDF + wc * (H / 4) + 16 * jc + (lane & 15)] =
-                acc[2 * p + ii][jc][e];
-      __syncthreads();
-      constexpr int NB = 1;  // rows per load batch (two do not fit the VGPR budget)
+    constexpr int NB = 2;  // rows per load batch: 2 x 7 loads of 16 B in flight per thread
 #pragma unroll 1
-      for (int kb = 0; kb < 64 / C::RPI; kb += NB) {
-        uint4 vin[NB][7];
+    for (int kb = 0; kb < 128 / C::RPI; kb += NB) {
+      uint4 vin[NB][7];
 #pragma unroll
-        for (int kk = 0; kk < NB; ++kk) {
-          const int ri = rsub + C::RPI * (kb + kk);
-          const int bl = (ri >> 5) * 64 + 32 * p + (ri & 31);  // row within the tile
-          const bool ok = m0 + bl < a.B;
-          const uint32_t oc = ok ? (uint32_t)(bl * H + jg) * 2u : 0x80000000u;
-          const uint32_t oy = ok ? (uint32_t)(bl * T_ * (int)a.ldy + jg) * 2u : 0x80000000u;
-          const uint32_t os = ok ? (uint32_t)(bl * T_ * 4 * H + jg) * 2u : 0x80000000u;
-          vin[kk][0] = ld16_buf(rc, oc, 0);
-          vin[kk][1] = ld16_buf(rd, oy, 0);
+      for (int kk = 0; kk < NB; ++kk) {
+        const int bl = rsub + C::RPI * (kb + kk);  // row within the tile
+        const bool ok = m0 + bl < a.B && !(dbg & 2);
+        const uint32_t oc = ok ? (uint32_t)(bl * H + jg) * 2u : 0x80000000u;
+        const uint32_t oy = ok ? (uint32_t)(bl * T_ * (int)a.ldy + jg) * 2u : 0x80000000u;
+        const uint32_t os = ok ? (uint32_t)(bl * T_ * 4 * H + jg) * 2u : 0x80000000u;
+        vin[kk][0] = ld16_buf(rc, oc, 0);
+        vin[kk][1] = ld16_buf(rd, oy, 0);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) vin[kk][2 + q] = ld16_buf(rsv, os, q * 2 * H);
-          vin[kk][6] = ld16_buf(ry, oy, 0);
-        }
-#pragma unroll
-        for (int kk = 0; kk < NB; ++kk) {
-          const int ri = rsub + C::RPI * (kb + kk);
-          const int bl = (ri >> 5) * 64 + 32 * p + (ri & 31);
-          const int b = m0 + bl;
-          if (b >= a.B) continue;
-          float cin[8], dy[8], ar[8], az[8], an[8], gh[8], hp[8];
-          unpack8(vin[kk][0], cin);
-          unpack8(vin[kk][1], dy);
-          unpack8(vin[kk][2], ar);
-          unpack8(vin[kk][3], az);
-          unpack8(vin[kk][4], an);
-          unpack8(vin[kk][5], gh);
-          unpack8(vin[kk][6], hp);
-          if (last && R.dfinal) ld8(R.dfinal + (long)b * a.ldf + jg, cin);  // fp32 final-state gradient
-          const float* Lc = L + ri * C::LDF + jg;
-          float o_r[8], o_z[8], o_n[8], o_hn[8], cout[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float dht = Lc[e] + cin[e] + dy[e];
-            float rg, omr, zg, omz, ng, sech2;
-            tt_sigmoid_pair(ar[e], rg, omr);
-            tt_sigmoid_pair(az[e], zg, omz);
-            tt_tanh_sech2(an[e], ng, sech2);
-            const float dnp = dht * omz * sech2;
-            const float drp = dnp * gh[e] * rg * omr;
-            const float dzp = dht * (hp[e] - ng) * zg * omz;
-            o_r[e] = drp; o_z[e] = dzp; o_n[e] = dnp; o_hn[e] = dnp * rg;
-            cout[e] = dht * zg;
-            bsum[0][e] += drp; bsum[1][e] += dzp; bsum[2][e] += dnp; bsum[3][e] += dnp * rg;
-          }
-          st8(cr_cur + (long)bl * H + jg, cout);
-          const long row = (long)b * T_ + t;
-          bf16_t* xw = DGXw + row * a.ldd + jg;
-          st8(xw, o_r);
-          st8(xw + H, o_z);
-          st8_sc1(grs, (int)(((long)bl * T_ * a.ldd + jg + 2 * H) * 2L), o_n, (bf16_t*)nullptr);
-          st8(DGHw + row * a.ldd + jg, o_hn);
-        }
+        for (int q = 0; q < 4; ++q) vin[kk][2 + q] = ld16_buf(rsv, os, q * 2 * H);
+        vin[kk][6] = ld16_buf(ry, oy, 0);
       }
-      __syncthreads();  // the image is rewritten by the next pass / the bias reduction
+#pragma unroll
+      for (int kk = 0; kk < NB; ++kk) {
+        const int bl = rsub + C::RPI * (kb + kk);
+        const int b = m0 + bl;
+        if (b >= a.B) continue;
+        float cin[8], dy[8], ar[8], az[8], an[8], gh[8], hp[8], gm[8];
+        unpack8(vin[kk][0], cin);
+        unpack8(vin[kk][1], dy);
+        unpack8(vin[kk][2], ar);
+        unpack8(vin[kk][3], az);
+        unpack8(vin[kk][4], an);
+        unpack8(vin[kk][5], gh);
+        unpack8(vin[kk][6], hp);
+        unpack8(*reinterpret_cast<const uint4*>(L16 + ((bl * C::LDB + jg) >> 1)), gm);
+        if (last && R.dfinal) ld8(R.dfinal + (long)b * a.ldf + jg, cin);  // fp32 final-state gradient
+        float o_r[8], o_z[8], o_n[8], o_hn[8], cout[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float dht = gm[e] + cin[e] + dy[e];
+          float rg, omr, zg, omz, ng, sech2;
+          tt_sigmoid_pair(ar[e], rg, omr);
+          tt_sigmoid_pair(az[e], zg, omz);
+          tt_tanh_sech2(an[e], ng, sech2);
+          const float dnp = dht * omz * sech2;
+          const float drp = dnp * gh[e] * rg * omr;
+          const float dzp = dht * (hp[e] - ng) * zg * omz;
+          o_r[e] = drp; o_z[e] = dzp; o_n[e] = dnp; o_hn[e] = dnp * rg;
+          cout[e] = dht * zg;
+          bsum[0][e] += drp; bsum[1][e] += dzp; bsum[2][e] += dnp; bsum[3][e] += dnp * rg;
+        }
+        if (dbg & 4) {
+          if (o_r[0] == 12345.f) L16[0] = __float_as_uint(o_z[1] + o_n[2] + o_hn[3] + cout[4]);
+          continue;
+        }
+        st8(cr_cur + (long)bl * H + jg, cout);
+        const long row = (long)b * T_ + t;
+        bf16_t* xw = DGXw + row * a.ldd + jg;
+        st8(xw, o_r);
+        st8(xw + H, o_z);
+        st8_sc1(grs, (int)(((long)bl * T_ * a.ldd + jg + 2 * H) * 2L), o_n, (bf16_t*)nullptr);
+        st8(DGHw + row * a.ldd + jg, o_hn);
+      }
     }
+    __syncthreads();  // the image is rewritten by the bias reduction
     // the step's bias partials: the RPI threads sharing each unit group meet in LDS, then
     // one add per column into the tile's partial row (owned by this workgroup alone)
     float* red = L;  // [RPI][4][H]

@@ -63,12 +63,49 @@ class GatherRows(torch.autograd.Function):
         return reduce_scatter_rows(g, ctx.group), None
 
 
+class OverlapReducer:
+    """Gradient buckets summed across ranks while the backward keeps running.
+
+    TowersFn.backward hands over the head + layer-1 gradients as soon as they exist
+    (launch) and runs the layer-0 BPTT while that all-reduce is on the wire; the layer-0
+    bucket follows, then finish() waits for both. Each bucket is one flat fp32
+    collective (RCCL: on its own stream, ordered after the kernels that produced the
+    bucket); the returned views of the reduced buffer become the parameters' gradients,
+    and the parameters are marked so allreduce_grads does not sum them a second time."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.works = []
+
+    def launch(self, grads):
+        flat = torch.cat([g.reshape(-1).float() for g in grads])
+        self.works.append(dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+        out, off = [], 0
+        for g in grads:
+            out.append(flat[off:off + g.numel()].view(g.shape))
+            off += g.numel()
+        return out
+
+    def finish(self, params=()):
+        for w in self.works:
+            w.wait()
+        self.works = []
+        for p in params:
+            p._tt_dp_reduced = True
+
+
 def allreduce_grads(params, group=None, bucket_bytes: int = 64 << 20):
     """Sum parameter gradients across ranks in flat buckets (one collective per
-    ~64 MB bucket: xGMI rings are per-link bound, so few large collectives win)."""
+    ~64 MB bucket: xGMI rings are per-link bound, so few large collectives win).
+    Gradients an OverlapReducer already summed during the backward are skipped."""
     if not active(group):
         return
-    grads = [p.grad for p in params if p.grad is not None]
+    grads = []
+    for p in params:
+        if getattr(p, "_tt_dp_reduced", False):
+            p._tt_dp_reduced = False
+        elif p.grad is not None:
+            grads.append(p.grad)
     bucket, size = [], 0
     for g in grads + [None]:
         if g is not None:

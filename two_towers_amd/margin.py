@@ -192,7 +192,8 @@ class TwoTowerModel(nn.Module):
         for e in encs:
             params.extend(getattr(e, n) for n in _GRU_ORDER)
         table = self._device_table(xs[0].device) if xs[0].dtype in (torch.int32, torch.int64) else None
-        return run_towers(cfg, table, xs, params)
+        return run_towers(cfg, table, xs, params, getattr(self, "process_group", None),
+                          getattr(self, "overlap_grad_allreduce", True) and torch.is_grad_enabled())
 
     def _project(self, vecs):
         """The shared projection over the row-stacked towers; returns one [B_i, H] per tower."""

@@ -35,6 +35,7 @@ class EnhancedTwoTowerModel(nn.Module):
         self.hidden_dim = hidden_dim
         self.compute_dtype = torch.float32
         self.process_group = None  # data-parallel group (None: the default group when initialised)
+        self.overlap_grad_allreduce = True  # DP: sum gradients across ranks inside the backward
         self._table = None  # not a parameter/buffer: keeps state_dict identical to the reference
 
     # ---------------------------------------------------------------- options
@@ -44,11 +45,15 @@ class EnhancedTwoTowerModel(nn.Module):
         self.compute_dtype = dtype
         return self
 
-    def set_process_group(self, group):
-        """Data-parallel group the batch is split over. Only the dropout masks depend on it:
+    def set_process_group(self, group, overlap_grad_allreduce: bool = True):
+        """Data-parallel group the batch is split over. The dropout masks depend on it:
         rank r's rows draw the masks of global rows r*B .. r*B+B-1, as one process running
-        the whole global batch would (so the ranks never repeat each other's masks)."""
+        the whole global batch would (so the ranks never repeat each other's masks). With
+        overlap_grad_allreduce the backward sums the gradients across the group itself,
+        the head + layer-1 bucket overlapping the layer-0 BPTT (dist.OverlapReducer);
+        dist.allreduce_grads then skips them."""
         self.process_group = group
+        self.overlap_grad_allreduce = overlap_grad_allreduce
         return self
 
     def set_embedding_table(self, table: torch.Tensor | None):
@@ -103,7 +108,8 @@ class EnhancedTwoTowerModel(nn.Module):
         for w in which:
             params.extend(self._tower_params(w))
         table = self._device_table(xs[0].device) if xs[0].dtype in (torch.int32, torch.int64) else None
-        return run_towers(cfg, table, xs, params)
+        return run_towers(cfg, table, xs, params, self.process_group,
+                          self.overlap_grad_allreduce and torch.is_grad_enabled())
 
     def encode_query(self, query_emb):
         return self._run(["query"], [query_emb])[0]

@@ -23,7 +23,7 @@ from dataclasses import dataclass
 import torch
 import torch.nn.functional as F
 
-from . import _lib, ops, timing
+from . import _lib, dist, ops, timing
 from ._lib import GruBwdRec, GruFwdRec, HeadBwdIO, HeadFwdIO, call, dtype_code, stream_ptr
 
 PARAMS_PER_TOWER = 22
@@ -248,7 +248,7 @@ class TowersFn(torch.autograd.Function):
     (cfg.head "none": margin_two_tower.py:59-61, the head runs outside)."""
 
     @staticmethod
-    def forward(ctx, cfg: TowerCfg, table, *args):
+    def forward(ctx, cfg: TowerCfg, table, group, *args):
         n = cfg.ntowers
         xs, params = args[:n], args[n:]
         _lib.require_gpu(*xs, *params)
@@ -273,6 +273,8 @@ class TowersFn(torch.autograd.Function):
             y = Y1[ti].view(B, T, 2 * H)
             hcat.append(torch.cat([y[:, T - 1, :H], y[:, 0, H:]], 1).to(HEAD_DT).contiguous())
         ctx.cfg = cfg
+        ctx.group = group
+        ctx.params = params
         ctx.dims = (B, T, Ep)
         ctx.seeds = seeds
         ctx.packs = packs
@@ -345,6 +347,13 @@ class TowersFn(torch.autograd.Function):
         dG1, dbih1, dbhh1 = _gru_layer_bwd(cfg, 1, B, T, S1, Y1, None, dhcat, packs)
         Xl1 = X1 if X1 is not None else Y0
         dWih1, dWhh1 = _weight_grads(cfg, B, T, dG1, Xl1, 2 * H, 2 * H, Y1)
+        gl = [{} for _ in range(n)]
+        _layer_grads(gl, 1, E, Ep, dWih1, dWhh1, dbih1, dbhh1)
+        # data-parallel: the head + layer-1 gradients are summed across ranks while the
+        # layer-0 BPTT below runs (dist.OverlapReducer)
+        red = dist.OverlapReducer(ctx.group[0]) if ctx.group is not None else None
+        if red is not None:
+            _reduce_into(red, gl, head_grads)
         # dL/dY0 = (dG1 Wih1) * dropout mask  [B*T, 2H]
         dY0 = [_alloc((B * T, 2 * H), dt, dev) for _ in range(n)]
         esz = 2 if dt == torch.bfloat16 else 4
@@ -363,28 +372,51 @@ class TowersFn(torch.autograd.Function):
         dG0, dbih0, dbhh0 = _gru_layer_bwd(cfg, 0, B, T, S0, Y0, dY0, None, packs)
         del dY0
         dWih0, dWhh0 = _weight_grads(cfg, B, T, dG0, X0, Ep, Ep, Y0)
+        gl0 = [{} for _ in range(n)]
+        _layer_grads(gl0, 0, E, Ep, dWih0, dWhh0, dbih0, dbhh0)
+        if red is not None:
+            _reduce_into(red, gl0, [[] for _ in range(n)])
+            red.finish(ctx.params)
         grads = []
         for ti in range(n):
-            gl = {}
-            for layer, (dWih, dWhh, dbih, dbhh) in enumerate(((dWih0, dWhh0, dbih0, dbhh0),
-                                                               (dWih1, dWhh1, dbih1, dbhh1))):
-                for d, sfx in enumerate(("", "_reverse")):
-                    w = dWih[ti][d]
-                    if layer == 0 and Ep != E:
-                        w = w[:, :E].contiguous()
-                    gl[f"weight_ih_l{layer}{sfx}"] = w
-                    gl[f"weight_hh_l{layer}{sfx}"] = dWhh[ti][d]
-                    gl[f"bias_ih_l{layer}{sfx}"] = dbih[ti][d].contiguous()
-                    gl[f"bias_hh_l{layer}{sfx}"] = dbhh[ti][d]
-            grads.extend(gl[k] for k in GRU_NAMES)
+            gl[ti].update(gl0[ti])
+            grads.extend(gl[ti][k] for k in GRU_NAMES)
             grads.extend(head_grads[ti])
         ctx.acts = None
         ctx.packs = None
-        return (None, None, *([None] * n), *grads)
+        ctx.params = None
+        return (None, None, None, *([None] * n), *grads)
 
 
-def run_towers(cfg: TowerCfg, table, xs, params):
+def _layer_grads(gl, layer, E, Ep, dWih, dWhh, dbih, dbhh):
+    """Per-tower {name: grad} of one GRU layer in the nn.GRU parameter layout."""
+    for ti in range(len(gl)):
+        for d, sfx in enumerate(("", "_reverse")):
+            w = dWih[ti][d]
+            if layer == 0 and Ep != E:
+                w = w[:, :E].contiguous()
+            gl[ti][f"weight_ih_l{layer}{sfx}"] = w
+            gl[ti][f"weight_hh_l{layer}{sfx}"] = dWhh[ti][d]
+            gl[ti][f"bias_ih_l{layer}{sfx}"] = dbih[ti][d].contiguous()
+            gl[ti][f"bias_hh_l{layer}{sfx}"] = dbhh[ti][d]
+
+
+def _reduce_into(red, gl, head_grads):
+    """Start one bucket's all-reduce and swap the gradients for views of the bucket."""
+    keys = [(ti, k) for ti in range(len(gl)) for k in gl[ti]]
+    heads = [(ti, j) for ti in range(len(head_grads)) for j in range(len(head_grads[ti]))]
+    views = red.launch([gl[ti][k] for ti, k in keys] + [head_grads[ti][j] for ti, j in heads])
+    for (ti, k), v in zip(keys, views):
+        gl[ti][k] = v
+    for (ti, j), v in zip(heads, views[len(keys):]):
+        head_grads[ti][j] = v
+
+
+def run_towers(cfg: TowerCfg, table, xs, params, reduce_group=None, reduce: bool = False):
+    """reduce: sum the gradients across the data-parallel reduce_group's ranks during the
+    backward (dist.OverlapReducer); ignored unless that group spans more than one rank."""
     if cfg.H % 8:
         raise ValueError(f"GRU hidden size {cfg.H} must be a multiple of 8 on the HIP path "
                          "(the step epilogues update 8 consecutive units per thread)")
-    return TowersFn.apply(cfg, table, *xs, *params)
+    group = (reduce_group,) if reduce and dist.active(reduce_group) else None
+    return TowersFn.apply(cfg, table, group, *xs, *params)

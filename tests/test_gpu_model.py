@@ -221,13 +221,15 @@ def test_big_tile_gru_backward_matches_step_kernel(B, T):
         assert cos > 0.9999 and rel(outs[1][k], outs[0][k]) < 2e-2, (k, cos)
 
 
+@pytest.mark.parametrize("r64", [0, 1])
 @pytest.mark.parametrize("h,B,T", [(256, 130, 5), (256, 520, 3), (128, 200, 6)])
-def test_row_owning_gru_backward_matches_step_kernels(h, B, T):
-    """bf16 backward through the persistent row-owning kernel (gru_bwd_rows: one launch
-    per layer, 128 rows x all H units per workgroup, H 512 / 256) vs the per-step launches
-    (option gru_bwd_persist = 0): the same arithmetic per element, so gradients agree to
-    accumulation order (the recurrent GEMM's K order and the bias partial sums differ).
-    B 130 / 520 / 200 give tail row tiles."""
+def test_row_owning_gru_backward_matches_step_kernels(h, B, T, r64):
+    """bf16 backward through the persistent row-owning kernels (one launch per layer,
+    H 512 / 256: gru_bwd_rows, 128 rows x all H units per workgroup; r64: gru_bwd_r64,
+    64 rows per workgroup, two per CU, second half of the grid started late) vs the
+    per-step launches (option gru_bwd_persist = 0): the same arithmetic per element, so
+    gradients agree to accumulation order (the recurrent GEMM's K order and the bias
+    partial sums differ). B 130 / 520 / 200 give tail row tiles."""
     E = 40
     g = torch.Generator().manual_seed(13)
     q = torch.randn(B, T, E, generator=g).to(DEV)
@@ -236,7 +238,7 @@ def test_row_owning_gru_backward_matches_step_kernels(h, B, T):
     for persist in (0, 1):
         m, _ = make_model(E, h, 5)
         m = m.to(DEV).train().set_compute_dtype(torch.bfloat16)
-        with option("gru_bwd_persist", persist):
+        with option("gru_bwd_persist", persist), option("gru_bwd_r64", r64), option("gru_bwd_phase", 2 * r64):
             qv, dv = m(q, d)
             loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
             loss.backward()

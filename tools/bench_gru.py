@@ -84,8 +84,11 @@ def main():
         if not v:
             continue
         rows, dbg, strm = (v.split(":") + ["0", "2"])[:3]
-        set_option("gru_bwd_persist", 1 if rows == "P" else 0)
-        set_option("gru_bwd_rows", 128 if rows == "P" else int(rows))
+        # P: gru_bwd_rows; R: gru_bwd_r64 with start delay `dbg` (gru_bwd_phase)
+        set_option("gru_bwd_persist", 1 if rows in ("P", "R") else 0)
+        set_option("gru_bwd_r64", 1 if rows == "R" else 0)
+        set_option("gru_bwd_phase", int(dbg) if rows == "R" else 0)
+        set_option("gru_bwd_rows", 128 if rows in ("P", "R") else int(rows))
         os.environ["TT_GRU_DBG"] = dbg  # read only by a -DTT_DIAG build
         set_option("gru_bwd_streams", int(strm))
         brecs, bkeep = setup_bwd(a.B, a.T, a.H, keep, dev)

@@ -24,6 +24,8 @@ enum Opt {
   OPT_GEMM_STREAM_OUT,  // 0: no write-through output stores
   OPT_HN_GEMM,          // 1: hard-negative top-k through GEMM + split top-k, no scan
   OPT_GRU_BWD_PERSIST,  // 0: per-step backward launches instead of the row-owning kernel
+  OPT_GRU_BWD_R64,      // 1: row-owning backward with 64-row workgroups, two per CU
+  OPT_GRU_BWD_PHASE,    // gru_bwd_r64: start delay of the grid's second half (s_sleep 127 units)
   OPT_N
 };
 int opt(Opt o);

@@ -32,7 +32,8 @@ constexpr OptDef kOpts[OPT_N] = {
     {"gru_bwd_big", "TT_GRU_BWD_BIG", 1},   {"gru_bwd_streams", "TT_GRU_BWD_STREAMS", 2},
     {"gemm_persist", "TT_GEMM_PERSIST", 1}, {"gemm_regstage", "TT_GEMM_REGSTAGE", 0},
     {"gemm_stream_out", "TT_GEMM_STREAM_OUT", 1}, {"hn_gemm", "TT_HN_GEMM", 0},
-    {"gru_bwd_persist", "TT_GRU_BWD_PERSIST", 1},
+    {"gru_bwd_persist", "TT_GRU_BWD_PERSIST", 1}, {"gru_bwd_r64", "TT_GRU_BWD_R64", 0},
+    {"gru_bwd_phase", "TT_GRU_BWD_PHASE", 0},
 };
 struct OptTable {
   std::atomic<int> v[OPT_N];

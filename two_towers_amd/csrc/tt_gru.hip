@@ -747,6 +747,250 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
   }
 }
 
+// ---- row-owning backward, 64 rows per workgroup, two workgroups per CU ------------
+// gru_bwd_rows runs one 512-thread workgroup per CU, so each CU alternates between its
+// MFMA phase (the recurrent product) and its HBM phase (the gate-gradient epilogue) with
+// nothing to fill the other unit. Here a workgroup owns 64 rows of one recurrence (256
+// threads, 80 KiB of LDS), two are resident per CU, and the second half of the grid
+// starts `phase` sleeps late, so the two run out of step: one's epilogue streams while
+// the other's product runs.
+//   Per step: acc[64 x H] = dL/dgh_{s+1}[64 x 3H] . W_hh[3H x H] in H/256 column passes
+//   (a pass's accumulator stays in registers; 4 waves x 64 columns, acc[4][4] each), each
+//   K-tile one LDS slot: A 64 rows x 128 B (8 KiB) + two 128-column W_hh sub-images
+//   (32 KiB), by LDS-DMA one K-tile ahead. The epilogue stages the whole accumulator as a
+//   bf16 [64][H+8] image and updates 8 units of one row per thread, as gru_bwd_rows.
+template <int H>
+struct BwdR64Cfg {
+  static constexpr int NP = H / 256;             // column passes per step
+  static constexpr int SLOT = 8192 + 2 * 16384;  // A + two B sub-images
+  static constexpr int LDS = 2 * SLOT;           // 80 KiB
+  static constexpr int TPR = H / 8;              // epilogue threads per row
+  static constexpr int RPI = 256 / TPR;          // rows per epilogue iteration
+  static constexpr int LDB = H + 8;              // staged bf16 row pitch
+  static_assert(64 * LDB * 2 <= LDS && RPI * 4 * H * 4 <= LDS, "staging fits the slots");
+};
+
+template <int H>
+__global__ __launch_bounds__(256, 2) void gru_bwd_r64(BwdArgs a, int phase) {
+  using C = BwdR64Cfg<H>;
+  __shared__ __attribute__((aligned(16))) char lds[C::LDS];
+  const int T_ = a.T, ntm = (a.B + 63) / 64;
+  const int id = ttg::xcd_remap(blockIdx.x, gridDim.x);
+  const int rz = id / ntm, mt = id - rz * ntm;
+  const BwdRec R = a.r[rz];
+  const int m0 = mt * 64;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const bf16_t* DGX = static_cast<const bf16_t*>(R.dgx);
+  const bf16_t* DGH = static_cast<const bf16_t*>(R.dgh);
+  bf16_t* DGXw = static_cast<bf16_t*>(R.dgx);
+  bf16_t* DGHw = static_cast<bf16_t*>(R.dgh);
+  const bf16_t* S = static_cast<const bf16_t*>(R.save);
+  const bf16_t* Y = static_cast<const bf16_t*>(R.y);
+  const bf16_t* DY = static_cast<const bf16_t*>(R.dy);
+  const bf16_t* W = static_cast<const bf16_t*>(R.whh);
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane(ttg::lds_addr_of(lds));
+  constexpr int NK = 3 * H / 64;  // K-tiles per pass
+  const long ldr = (long)T_ * a.ldd;  // elements between batch rows of dgx / dgh
+  // DMA pieces (1 KiB per wave-instruction). A: pieces wave + 4j (j < 2) of the 8 KiB KC
+  // image; per thread the row and the source chunk its LDS slot holds.
+  int arow[2], acol[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int p = (wave + 4 * j) * 64 + lane, row = p >> 3;
+    arow[j] = row;
+    acol[j] = ((p & 7) ^ ((row >> 1) & 7)) * 8;
+  }
+  // B: pieces wave + 4j (j < 4) of each 16 KiB KO sub-image: k-row and source column
+  int boff[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int p = (wave + 4 * j) * 64 + lane, kl = p >> 4, q = p & 15;
+    boff[j] = kl * H + (q ^ (ttg::ko_v(kl) << 1)) * 8;
+  }
+  const int jg = (tid % C::TPR) * 8, rsub = tid / C::TPR;
+  float* L = reinterpret_cast<float*>(lds);
+  float* part = R.dbias + (long)mt * (4L * H);  // this tile's partial row (zeroed by the host)
+
+  if (blockIdx.x >= gridDim.x / 2)  // second resident workgroup of a CU: start out of step
+    for (int i = 0; i < phase; ++i) __builtin_amdgcn_s_sleep(127);
+
+  for (int s = T_ - 1; s >= 0; --s) {
+    const int t = R.dir ? T_ - 1 - s : s;
+    const int tn = R.dir ? t - 1 : t + 1;
+    const int tp = R.dir ? t + 1 : t - 1;
+    const bool last = (s == T_ - 1);
+    f32x4 acc[C::NP][4][4];
+#pragma unroll
+    for (int p = 0; p < C::NP; ++p)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[p][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (!last) {
+      // A rows: this workgroup's own dL/dgh_{s+1} (r|z columns from dgx, n from dgh)
+      const char* asrc[2][2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int b = m0 + arow[j];
+        const bool ok = b < a.B;
+        asrc[j][0] = ok ? reinterpret_cast<const char*>(DGX + (long)tn * a.ldd + (long)b * ldr + acol[j])
+                        : reinterpret_cast<const char*>(ttg::g_tt_zero_page);
+        asrc[j][1] = ok ? reinterpret_cast<const char*>(DGH + (long)tn * a.ldd + (long)b * ldr + acol[j] - 2 * H)
+                        : reinterpret_cast<const char*>(ttg::g_tt_zero_page);
+      }
+      // K-tile `it` (pass it / NK, K-tile it % NK) into slot image `img`
+      auto issue = [&](int it, uint32_t img) {
+        const int p = it / NK, r = it - p * NK;
+        const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const bool hi = r * 64 >= 2 * H;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const char* src = asrc[j][hi ? 1 : 0];
+          if (src != reinterpret_cast<const char*>(ttg::g_tt_zero_page)) src += (long)r * ttg::KTB;
+          ttg::dma16(src, img + (uint32_t)(wv + 4 * j) * 1024u);
+        }
+        const bf16_t* wb = W + (long)r * 64 * H + p * 256;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            ttg::dma16(wb + q * 128 + boff[j], img + 8192u + 16384u * q + (uint32_t)(wv + 4 * j) * 1024u);
+      };
+      constexpr int NIT = C::NP * NK;
+      issue(0, lbase);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+#pragma unroll 1
+      for (int it = 0; it < NIT; ++it) {
+        const int cs = it & 1;
+        const char* sl = lds + cs * C::SLOT;
+        if (it + 1 < NIT) issue(it + 1, lbase + (cs ^ 1) * C::SLOT);
+        const char* ib = sl + 8192 + (wave >> 1) * 16384;
+        const int cb = (wave & 1) * 64;
+        const int p = it / NK;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {  // one 32-deep half at a time: 32 fragment registers
+          uint4 fa[4], fb[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) fa[i] = ttg::frag<bf16_t, false>(sl, 16 * i, ks);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) fb[j] = ttg::frag<bf16_t, true>(ib, cb + 16 * j, ks);
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int pp = 0; pp < C::NP; ++pp) {
+            if (pp != p) continue;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) acc[pp][i][j] = ttg::mma<bf16_t>(fa[i], fb[j], acc[pp][i][j]);
+          }
+          __builtin_amdgcn_s_setprio(0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of K-tile it+1
+        __builtin_amdgcn_s_barrier();                      // everyone's; slot cs is free
+      }
+    }
+    // ---- epilogue (as gru_bwd_rows): the accumulator as a bf16 [64][LDB] image
+    const long trow = (long)m0 * T_ + t;
+    const __amdgpu_buffer_rsrc_t rc =
+        tt_rsrc_n(static_cast<const bf16_t*>(R.dh) + (long)((s + 1) & 1) * a.B * H + (long)m0 * H, !last);
+    bf16_t* cr_cur = static_cast<bf16_t*>(R.dh) + (long)(s & 1) * a.B * H + (long)m0 * H;
+    const __amdgpu_buffer_rsrc_t rd = tt_rsrc_n(DY ? DY + trow * a.ldy : S, DY != nullptr);
+    const __amdgpu_buffer_rsrc_t rsv = tt_rsrc_n(S + trow * 4L * H, true);
+    const __amdgpu_buffer_rsrc_t ry = tt_rsrc_n(s > 0 ? Y + ((long)m0 * T_ + tp) * a.ldy : S, s > 0);
+    const __amdgpu_buffer_rsrc_t grs = tt_rsrc(DGXw + trow * a.ldd);
+    uint32_t* L16 = reinterpret_cast<uint32_t*>(lds);
+#pragma unroll
+    for (int p = 0; p < C::NP; ++p)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            reinterpret_cast<bf16_t*>(lds)[(16 * i + 4 * (lane >> 4) + e) * C::LDB + p * 256 + wave * 64 + 16 * j +
+                                           (lane & 15)] = f2bf(acc[p][i][j][e]);
+    __syncthreads();
+    float bsum[4][8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bsum[q][e] = 0.f;
+    constexpr int NB = 2;
+#pragma unroll 1
+    for (int kb = 0; kb < 64 / C::RPI; kb += NB) {
+      uint4 vin[NB][7];
+#pragma unroll
+      for (int kk = 0; kk < NB; ++kk) {
+        const int bl = rsub + C::RPI * (kb + kk);
+        const bool ok = m0 + bl < a.B;
+        const uint32_t oc = ok ? (uint32_t)(bl * H + jg) * 2u : 0x80000000u;
+        const uint32_t oy = ok ? (uint32_t)(bl * T_ * (int)a.ldy + jg) * 2u : 0x80000000u;
+        const uint32_t os = ok ? (uint32_t)(bl * T_ * 4 * H + jg) * 2u : 0x80000000u;
+        vin[kk][0] = ld16_buf(rc, oc, 0);
+        vin[kk][1] = ld16_buf(rd, oy, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) vin[kk][2 + q] = ld16_buf(rsv, os, q * 2 * H);
+        vin[kk][6] = ld16_buf(ry, oy, 0);
+      }
+#pragma unroll
+      for (int kk = 0; kk < NB; ++kk) {
+        const int bl = rsub + C::RPI * (kb + kk);
+        const int b = m0 + bl;
+        if (b >= a.B) continue;
+        float cin[8], dy[8], ar[8], az[8], an[8], gh[8], hp[8], gm[8];
+        unpack8(vin[kk][0], cin);
+        unpack8(vin[kk][1], dy);
+        unpack8(vin[kk][2], ar);
+        unpack8(vin[kk][3], az);
+        unpack8(vin[kk][4], an);
+        unpack8(vin[kk][5], gh);
+        unpack8(vin[kk][6], hp);
+        unpack8(*reinterpret_cast<const uint4*>(L16 + ((bl * C::LDB + jg) >> 1)), gm);
+        if (last && R.dfinal) ld8(R.dfinal + (long)b * a.ldf + jg, cin);
+        float o_r[8], o_z[8], o_n[8], o_hn[8], cout[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float dht = gm[e] + cin[e] + dy[e];
+          float rg, omr, zg, omz, ng, sech2;
+          tt_sigmoid_pair(ar[e], rg, omr);
+          tt_sigmoid_pair(az[e], zg, omz);
+          tt_tanh_sech2(an[e], ng, sech2);
+          const float dnp = dht * omz * sech2;
+          const float drp = dnp * gh[e] * rg * omr;
+          const float dzp = dht * (hp[e] - ng) * zg * omz;
+          o_r[e] = drp; o_z[e] = dzp; o_n[e] = dnp; o_hn[e] = dnp * rg;
+          cout[e] = dht * zg;
+          bsum[0][e] += drp; bsum[1][e] += dzp; bsum[2][e] += dnp; bsum[3][e] += dnp * rg;
+        }
+        st8(cr_cur + (long)bl * H + jg, cout);
+        const long row = (long)b * T_ + t;
+        bf16_t* xw = DGXw + row * a.ldd + jg;
+        st8(xw, o_r);
+        st8(xw + H, o_z);
+        st8_sc1(grs, (int)(((long)bl * T_ * a.ldd + jg + 2 * H) * 2L), o_n, (bf16_t*)nullptr);
+        st8(DGHw + row * a.ldd + jg, o_hn);
+      }
+    }
+    __syncthreads();  // the image is rewritten by the bias reduction
+    float* red = L;  // [RPI][4][H]
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[(rsub * 4 + q) * H + jg + e] = bsum[q][e];
+    __syncthreads();
+    for (int c = tid; c < 4 * H; c += 256) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < C::RPI; ++w) v += red[w * 4 * H + c];
+      part[c] += v;
+    }
+    // this step's dL/dgh and carry feed the next iteration's DMA
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+}
+
 // ---- persistent ("row-resident") forward, bf16 ---------------------------------
 // Batch rows never interact, so one workgroup can own 64 rows of one recurrence for
 // all T steps: h_{s-1} stays in LDS as the A operand (bf16 KC image, never re-read
@@ -1070,7 +1314,11 @@ bool gru_fwd_persistent(int dtype, int H) {
 // batch rows per backward tile: 128, or 64 with option gru_bwd_rows = 64 (3 workgroups
 // per CU; measured slower at B=8192, H=512: 13.6 vs 11.5 ms per layer)
 static int bwd_rows() { return tt::opt(tt::OPT_GRU_BWD_ROWS) == 64 ? 64 : 128; }
-extern "C" int tt_gru_bias_rows(int B) { return tt_ceil_div(B, bwd_rows()); }
+// partial bias rows: one per backward row tile (64 rows with gru_bwd_r64; extra rows of
+// a smaller-tile count are zero-filled by tt_gru_bwd and add nothing)
+extern "C" int tt_gru_bias_rows(int B) {
+  return tt_ceil_div(B, tt::opt(tt::OPT_GRU_BWD_R64) ? 64 : bwd_rows());
+}
 
 extern "C" int tt_gru_fwd_launches(int dtype, int T, int H) { return gru_fwd_persistent(dtype, H) ? 1 : T; }
 
@@ -1172,6 +1420,14 @@ extern "C" int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B
   // launches)
   if (gru_bwd_persistent(dtype, H)) {
     TT_CHECK_ARG(128L * T * std::max({ldd, ldy, 4L * H}) * esz < (1L << 31), "tt_gru_bwd: tile offsets exceed 2 GiB");
+    if (tt::opt(tt::OPT_GRU_BWD_R64)) {
+      const dim3 grid(tt_ceil_div(B, 64) * nrec);
+      const int ph = std::max(0, tt::opt(tt::OPT_GRU_BWD_PHASE));
+      if (H == 512) hipLaunchKernelGGL(gru_bwd_r64<512>, grid, dim3(256), 0, st, a, ph);
+      else hipLaunchKernelGGL(gru_bwd_r64<256>, grid, dim3(256), 0, st, a, ph);
+      TT_CHECK_LAUNCH("gru_bwd_r64");
+      return 0;
+    }
     const dim3 grid(tt_ceil_div(B, 128) * nrec);
     if (H == 512) hipLaunchKernelGGL(gru_bwd_rows<512>, grid, dim3(512), 0, st, a);
     else hipLaunchKernelGGL(gru_bwd_rows<256>, grid, dim3(512), 0, st, a);

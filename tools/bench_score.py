@@ -57,14 +57,19 @@ def infonce(B, nd, h, dt, iters):
     f()
     dq = torch.empty(B, h, device="cuda")
     dd = torch.empty(nd, h, device="cuda")
-    wsb = torch.empty(max(lib.tt_infonce_bwd_ws_size(dtype_code(dt), B, nd, h), 1), dtype=torch.uint8, device="cuda")
     gs = torch.tensor([1.0 / B], device="cuda")
-    fb = lambda: call("tt_infonce_bwd", dtype_code(dt), q.data_ptr(), B, d.data_ptr(), nd, h, 1.0 / 0.07, 0.0, 0,
-                      lse.data_ptr(), gs.data_ptr(), dq.data_ptr(), dd.data_ptr(), wsb.data_ptr(), st)
-    msb = timed(fb, iters)
-    tfb = 6.0 * B * nd * h / (msb * 1e-3) / 1e12
-    print(json.dumps({"op": "infonce_bwd", "B": B, "nd": nd, "h": h, "dtype": str(dt)[6:], "ms": round(msb, 4),
-                      "tflops": round(tfb, 1), "mfma_frac": round(tfb / 2500.0, 4)}), flush=True)
+    for flash in (1, 0):  # fused (no dS) vs materialised dS
+        with _lib.option("infonce_flash", flash):
+            wsb = torch.empty(max(lib.tt_infonce_bwd_ws_size(dtype_code(dt), B, nd, h), 1), dtype=torch.uint8,
+                              device="cuda")
+            fb = lambda: call("tt_infonce_bwd", dtype_code(dt), q.data_ptr(), B, d.data_ptr(), nd, h, 1.0 / 0.07,
+                              0.0, 0, lse.data_ptr(), gs.data_ptr(), dq.data_ptr(), dd.data_ptr(), wsb.data_ptr(), st)
+            msb = timed(fb, iters)
+        tfb = 6.0 * B * nd * h / (msb * 1e-3) / 1e12
+        print(json.dumps({"op": "infonce_bwd", "flash": flash, "B": B, "nd": nd, "h": h, "dtype": str(dt)[6:],
+                          "ms": round(msb, 4), "ws_bytes": wsb.numel(), "tflops": round(tfb, 1),
+                          "mfma_frac": round(tfb / 2500.0, 4)}), flush=True)
+        del wsb
     return {"op": "infonce_fwd", "B": B, "nd": nd, "h": h, "dtype": str(dt)[6:], "ms": round(ms, 4),
             "tflops": round(tf, 1), "mfma_frac": round(tf / 2500.0, 4)}
 

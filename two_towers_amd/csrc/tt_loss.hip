@@ -202,6 +202,208 @@ __global__ __launch_bounds__(256) void infonce_dscore_kernel(const T* __restrict
   });
 }
 
+// ---------------------------------------------- fused InfoNCE backward, bf16, no dS
+// dS[i][j] = g * (softmax_ij - [j == label_i]) is recomputed tile by tile and consumed
+// in LDS; nothing of size B x N is written. Two roles of one kernel:
+//   OWNQ : a workgroup owns 128 query rows i and sweeps document tiles j:
+//          dq_i  = inv_tau * sum_j dS_ij d_j
+//   !OWNQ: a workgroup owns 128 document rows j and sweeps query tiles i:
+//          dd_j  = inv_tau * sum_i dS_ij q_i
+// Per 64-row tile of the swept operand X: S = O . X^T (MFMA over K = H, own rows and the
+// tile staged in LDS as K-contig images), dS -> LDS as the bf16 A operand, then
+// dO += dS . X with X's K-contig image read as the K-outer B operand by transposing
+// reads (ds_read_b64_tr_b16), so each X tile is loaded once for both products. X tiles are
+// LDS-DMA'd one tile ahead. A sweep may be split over workgroups (fp32 partial slabs,
+// summed by infonce_slab_sum_kernel).
+//   LDS (H = 256): own rows 64 KiB + two X tiles 2 x 32 KiB + dS 16 KiB = 144 KiB.
+// 8 waves as 4 (own rows) x 2: product 1 wave tile 32 x 32, product 2 wave tile 32 x H/2.
+template <int H>
+struct FlashCfg {
+  static constexpr int NKT = H / 64;            // K-tiles of 64 features
+  static constexpr int OWN = 128 * 128 * NKT;   // own-row images (128 rows x 128 B each)
+  static constexpr int XT = 64 * 128 * NKT;     // one X tile
+  static constexpr int DS = 128 * 128;          // dS: 128 own rows x 64 tile rows (one K-tile)
+  static constexpr int LDS = OWN + 2 * XT + DS;
+  static constexpr int NO = H / 32;             // 16-column MFMA tiles per wave, product 2
+};
+
+// MFMA B fragment of X^T . (k = tile row, n = feature) from the K-contig X image of feature
+// K-tile `img` (rows of 128 B, 16-B chunk c of row k at c ^ ((k >> 1) & 7)): the reads of
+// frag<bf16, true>, addressed into this layout.
+TT_DEV uint4 frag_kc_tr(const char* img, int n0, int ks) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, i4 = lane & 15, q = i4 >> 2, p = i4 & 3;
+  const int k0 = ks * 32 + 8 * g + q, k1 = k0 + 4;
+  const int n = n0 + 4 * p;
+  const int o0 = k0 * 128 + ((((n >> 3) & 7) ^ ((k0 >> 1) & 7)) << 4) + ((n >> 2) & 1) * 8;
+  const int o1 = k1 * 128 + ((((n >> 3) & 7) ^ ((k1 >> 1) & 7)) << 4) + ((n >> 2) & 1) * 8;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + o0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + o1));
+  uint4 v;
+  v.x = (uint32_t)(uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16);
+  v.y = (uint32_t)(uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16);
+  v.z = (uint32_t)(uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16);
+  v.w = (uint32_t)(uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16);
+  return v;
+}
+
+// rows [r0, r0 + nrows_img) of a row-major bf16 [rows][H] matrix -> K-contig images (one
+// per 64-feature K-tile, 128 B per row), by LDS-DMA; rows past `rows` read the zero page
+template <int H>
+TT_DEV void flash_stage(const bf16_t* src, long rows, long r0, int nrows_img, uint32_t img) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int pieces = nrows_img * 128 / 1024;  // 1 KiB pieces per K-tile image
+  for (int kt = 0; kt < H / 64; ++kt)
+    for (int pc = wave; pc < pieces; pc += 8) {
+      const int p = pc * 64 + lane, row = p >> 3, c = (p & 7) ^ ((row >> 1) & 7);
+      const long gr = r0 + row;
+      const void* s = gr < rows ? static_cast<const void*>(src + gr * H + kt * 64 + c * 8)
+                                : static_cast<const void*>(ttg::g_tt_zero_page);
+      ttg::dma16(s, img + (uint32_t)(kt * nrows_img * 128 + pc * 1024));
+    }
+}
+
+template <int H, bool OWNQ>
+__global__ __launch_bounds__(512) void infonce_bwd_flash_kernel(const bf16_t* __restrict__ qn, long bq,
+                                                                const bf16_t* __restrict__ dn, long nd, float inv_tau,
+                                                                float offdiag, long label_off,
+                                                                const float* __restrict__ lse,
+                                                                const float* __restrict__ gscale, int tiles_per_split,
+                                                                float* __restrict__ out) {
+  using C = FlashCfg<H>;
+  __shared__ __attribute__((aligned(16))) char lds[C::LDS];
+  const float gs = gscale ? *gscale : 1.f;
+  const bf16_t* O = OWNQ ? qn : dn;
+  const bf16_t* X = OWNQ ? dn : qn;
+  const long nown = OWNQ ? bq : nd, nx = OWNQ ? nd : bq;
+  const long o0 = (long)blockIdx.y * 128;
+  const long ntile = (nx + 63) / 64;
+  const long t0 = (long)blockIdx.x * tiles_per_split, t1 = std::min(ntile, t0 + tiles_per_split);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;  // product 1: own rows x tile rows
+  const int wf = (wave & 1) * (H / 2);                    // product 2: feature columns
+  const uint32_t lb = __builtin_amdgcn_readfirstlane(ttg::lds_addr_of(lds));
+  char* dsimg = lds + C::OWN + 2 * C::XT;
+  f32x4 acc_o[2][C::NO];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < C::NO; ++j) acc_o[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // per own row (product-1 layout: rows wm + 16i + 4(lane>>4) + r): its lse when OWNQ
+  float lown[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long row = o0 + wm + 16 * i + 4 * (lane >> 4) + r;
+      lown[i][r] = (OWNQ && row < nown) ? lse[row] : 0.f;
+    }
+  if (t0 < t1) {
+    flash_stage<H>(O, nown, o0, 128, lb);
+    flash_stage<H>(X, nx, t0 * 64, 64, lb + C::OWN);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (long t = t0; t < t1; ++t) {
+    const int cur = (int)((t - t0) & 1);
+    const char* xi = lds + C::OWN + cur * C::XT;
+    if (t + 1 < t1) flash_stage<H>(X, nx, (t + 1) * 64, 64, lb + C::OWN + (cur ^ 1) * C::XT);
+    // product 1: S tile [128 own x 64 tile rows]
+    f32x4 acc_s[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc_s[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < C::NKT; ++kt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        uint4 fa[2], fb[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) fa[i] = ttg::frag<bf16_t, false>(lds + kt * 128 * 128, wm + 16 * i, ks);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb[j] = ttg::frag<bf16_t, false>(xi + kt * 64 * 128, wn + 16 * j, ks);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc_s[i][j] = ttg::mma<bf16_t>(fa[i], fb[j], acc_s[i][j]);
+      }
+    // dS (own row, tile row) -> bf16 K-contig image [128 own rows][64 tile rows]
+    float lx[2] = {0.f, 0.f};
+    if (!OWNQ) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const long xr = t * 64 + wn + 16 * j + (lane & 15);
+        lx[j] = xr < nx ? lse[xr] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int orl = wm + 16 * i + 4 * (lane >> 4) + r, xcl = wn + 16 * j + (lane & 15);
+          const long orow = o0 + orl, xrow = t * 64 + xcl;
+          const long qi = OWNQ ? orow : xrow, dj = OWNQ ? xrow : orow;
+          const bool lab = dj == label_off + qi;
+          float s = acc_s[i][j][r] * inv_tau;
+          if (!lab) s -= offdiag;
+          const float p = __expf(s - (OWNQ ? lown[i][r] : lx[j]));
+          const float v = (orow < nown && xrow < nx) ? gs * (p - (lab ? 1.f : 0.f)) : 0.f;
+          *reinterpret_cast<bf16_t*>(dsimg + orl * 128 + ((((xcl >> 3) ^ ((orl >> 1) & 7))) << 4) + (xcl & 7) * 2) =
+              f2bf(v);
+        }
+    __syncthreads();
+    // product 2: dO[128 own x H] += dS[128 x 64] . X[64 x H]
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 fa[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = ttg::frag<bf16_t, false>(dsimg, wm + 16 * i, ks);
+#pragma unroll
+      for (int j = 0; j < C::NO; ++j) {
+        const int f = wf + 16 * j;
+        const uint4 fb = frag_kc_tr(xi + (f >> 6) * 64 * 128, f & 63, ks);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc_o[i][j] = ttg::mma<bf16_t>(fa[i], fb, acc_o[i][j]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile t+1
+    __syncthreads();                                   // everyone's; dS and tile t are free
+  }
+  // out: [splits][nown][H] fp32 slab of this split (or the final array when unsplit)
+  float* dst = out + (long)blockIdx.x * nown * H;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long row = o0 + wm + 16 * i + 4 * (lane >> 4) + r;
+      if (row >= nown) continue;
+#pragma unroll
+      for (int j = 0; j < C::NO; ++j) dst[row * H + wf + 16 * j + (lane & 15)] = acc_o[i][j][r] * inv_tau;
+    }
+}
+
+__global__ __launch_bounds__(256) void infonce_slab_sum_kernel(const float* __restrict__ slab, int splits, long n,
+                                                               float* __restrict__ out) {
+  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= n) return;
+  float4 a = *reinterpret_cast<const float4*>(slab + i);
+  for (int s = 1; s < splits; ++s) {
+    const float4 b = *reinterpret_cast<const float4*>(slab + (long)s * n + i);
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  *reinterpret_cast<float4*>(out + i) = a;
+}
+
+// sweep splits per role: enough workgroups to cover the 256 CUs
+inline int flash_splits(long nown, long nx) {
+  const long blocks = (nown + 127) / 128, ntile = (nx + 63) / 64;
+  return (int)std::max<long>(1, std::min<long>(ntile, 256 / std::max<long>(blocks, 1)));
+}
+inline bool flash_ok(int dtype, int h) { return dtype == TT_DT_BF16 && (h == 128 || h == 256); }
+
 constexpr int TOPK_MAX = ttk::SK_MAX;
 
 // ---------------------------------------------------------------- margin loss
@@ -455,9 +657,39 @@ extern "C" int tt_infonce_fwd(int dtype, const void* qn, long bq, const void* dn
   return 0;
 }
 
+static bool use_flash(int dtype, int h) { return flash_ok(dtype, h) && tt::opt(tt::OPT_INFONCE_FLASH) != 0; }
+
 extern "C" long tt_infonce_bwd_ws_size(int dtype, long bq, long nd, int h) {
+  if (use_flash(dtype, h)) {  // fp32 partial slabs of split sweeps (none when unsplit)
+    const int sq = flash_splits(bq, nd), sd = flash_splits(nd, bq);
+    const long a = sq > 1 ? (long)sq * bq * h : 0, b = sd > 1 ? (long)sd * nd * h : 0;
+    return std::max<long>(256, std::max(a, b) * (long)sizeof(float));
+  }
   InfoWs w;
   return infonce_ws(dtype, bq, nd, h, &w);
+}
+
+// one role of the fused backward: out = dq (OWNQ) or dd, through slabs when split
+template <int H, bool OWNQ>
+static int flash_role(const bf16_t* qn, long bq, const bf16_t* dn, long nd, float inv_tau, float offdiag,
+                      long label_off, const float* lse, const float* gscale, float* out, float* slab,
+                      hipStream_t st) {
+  const long nown = OWNQ ? bq : nd, nx = OWNQ ? nd : bq;
+  const long ntile = (nx + 63) / 64;
+  int splits = flash_splits(nown, nx);
+  const int per = tt_ceil_div(ntile, splits);
+  splits = tt_ceil_div(ntile, per);
+  const dim3 grid((unsigned)splits, (unsigned)tt_ceil_div(nown, 128));
+  hipLaunchKernelGGL((infonce_bwd_flash_kernel<H, OWNQ>), grid, dim3(512), 0, st, qn, bq, dn, nd, inv_tau, offdiag,
+                     label_off, lse, gscale, per, splits > 1 ? slab : out);
+  TT_CHECK_LAUNCH("infonce_bwd_flash_kernel");
+  if (splits > 1) {
+    const long n = nown * H;
+    hipLaunchKernelGGL(infonce_slab_sum_kernel, dim3((unsigned)tt_ceil_div(n / 4, 256)), dim3(256), 0, st, slab,
+                       splits, n, out);
+    TT_CHECK_LAUNCH("infonce_slab_sum_kernel");
+  }
+  return 0;
 }
 
 extern "C" int tt_infonce_bwd(int dtype, const void* qn, long bq, const void* dn, long nd, int h, float inv_tau,
@@ -467,6 +699,21 @@ extern "C" int tt_infonce_bwd(int dtype, const void* qn, long bq, const void* dn
   TT_CHECK_ARG(label_offset >= 0 && label_offset + bq <= nd, "tt_infonce_bwd: labels outside [0, nd)");
   if (bq == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  if (use_flash(dtype, h)) {
+    TT_CHECK_ARG((((uintptr_t)qn | (uintptr_t)dn) & 15) == 0, "tt_infonce_bwd: bf16 rows must be 16-byte aligned");
+    TT_CHECK_ARG(ws != nullptr && bq <= 65535L * 128 && nd <= 65535L * 128, "tt_infonce_bwd: workspace/size");
+    const bf16_t* q = static_cast<const bf16_t*>(qn);
+    const bf16_t* d = static_cast<const bf16_t*>(dn);
+    float* slab = static_cast<float*>(ws);
+    if (h == 256) {
+      TT_PROPAGATE((flash_role<256, true>(q, bq, d, nd, inv_tau, offdiag_sub, label_offset, lse, gscale, dqn, slab, st)));
+      TT_PROPAGATE((flash_role<256, false>(q, bq, d, nd, inv_tau, offdiag_sub, label_offset, lse, gscale, ddn, slab, st)));
+    } else {
+      TT_PROPAGATE((flash_role<128, true>(q, bq, d, nd, inv_tau, offdiag_sub, label_offset, lse, gscale, dqn, slab, st)));
+      TT_PROPAGATE((flash_role<128, false>(q, bq, d, nd, inv_tau, offdiag_sub, label_offset, lse, gscale, ddn, slab, st)));
+    }
+    return 0;
+  }
   InfoWs w;
   infonce_ws(dtype, bq, nd, h, &w);
   char* base = static_cast<char*>(ws);

@@ -247,3 +247,46 @@ def test_row_owning_gru_backward_matches_step_kernels(h, B, T, r64):
         a, b = outs[1][k].double(), outs[0][k].double()
         cos = float((a * b).sum() / (a.norm() * b.norm() + 1e-30))
         assert cos > 0.9999 and rel(outs[1][k], outs[0][k]) < 2e-2, (k, cos)
+
+
+def test_packed_weight_cache_follows_parameter_versions():
+    """Inference calls reuse the packed compute copies of the weights (towers._packed)
+    while the parameters are unchanged, and repack after an optimizer step
+    (two_towers_amd.Adam bumps the versions) or load_state_dict: outputs always equal a
+    freshly built model holding the same weights."""
+    E, h, B, T = 32, 16, 40, 6
+    m, _ = make_model(E, h, 21)
+    m = m.to(DEV).set_compute_dtype(torch.bfloat16)
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(B, T, E, generator=g).to(DEV)
+    y = torch.randn(B, T, E, generator=g).to(DEV)
+    p0 = m.query_encoder.weight_ih_l0
+
+    def fresh_out():
+        f, _ = make_model(E, h, 0)
+        f.load_state_dict(m.state_dict())
+        f = f.to(DEV).set_compute_dtype(torch.bfloat16).eval()
+        with torch.no_grad():
+            return f.encode_query(x)
+
+    m.eval()
+    with torch.no_grad():
+        a = m.encode_query(x)
+        pk = p0._tt_pack[1]
+        b = m.encode_query(x)
+    assert p0._tt_pack[1] is pk and torch.equal(a, b)
+    m.train()
+    opt = tta.Adam(m.parameters(), lr=1e-2)
+    qv, dv = m(x, y)
+    tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv).backward()
+    opt.step()
+    m.eval()
+    with torch.no_grad():
+        c = m.encode_query(x)
+    assert p0._tt_pack[1] is not pk and not torch.equal(c, a)
+    assert torch.equal(c, fresh_out())
+    sd = {k: v + 0.01 for k, v in m.state_dict().items()}
+    m.load_state_dict(sd)
+    with torch.no_grad():
+        d = m.encode_query(x)
+    assert torch.equal(d, fresh_out())

@@ -299,6 +299,14 @@ def test_pair_id_batches_shard_global_batches(tmp_path):
     assert len(r0) == len(r1) == 103 // 8
     for a, b, g in zip(r0, r1, full):  # the two ranks' rows are exactly the global batch
         assert sorted(map(tuple, torch.cat([a, b]).tolist())) == sorted(map(tuple, g.tolist()))
+    assert len({tuple(q.flatten().tolist()) for q in full}) == len(full)  # no aliased batches
+    # world > 1: the ragged last global batch is dropped even with drop_last=False, so
+    # every rank's slices stay equal (the DP collectives need equal shapes)
+    r0 = [q for q, _ in ds.batches(4, device="cpu", seed=3, rank=0, world=2, drop_last=False)]
+    r1 = [q for q, _ in ds.batches(4, device="cpu", seed=3, rank=1, world=2, drop_last=False)]
+    assert len(r0) == len(r1) == 103 // 8 and all(q.shape[0] == 4 for q in r0 + r1)
+    tail = [q for q, _ in ds.batches(8, device="cpu", seed=3, world=1, drop_last=False)]
+    assert len(tail) == 103 // 8 + 1 and tail[-1].shape[0] == 103 % 8
 
 
 def test_read_pairs_formats(tmp_path):

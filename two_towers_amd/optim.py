@@ -56,4 +56,7 @@ class Adam(torch.optim.Optimizer):
                          arr([self.state[p]["exp_avg"] for p in chunk]),
                          arr([self.state[p]["exp_avg_sq"] for p in chunk]), sizes, n, group["lr"], b1, b2,
                          group["eps"], group["weight_decay"], step, stream_ptr(chunk[0].device))
+            # the kernel writes through raw pointers: record the in-place update for autograd
+            # and for the packed-weight cache of the towers (towers._packed)
+            torch.autograd.graph.increment_version(ps)
         return loss

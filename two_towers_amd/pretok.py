@@ -142,26 +142,39 @@ class PairIds(Dataset):
                 rank: int = 0, world: int = 1) -> Iterator[Tuple[torch.Tensor, torch.Tensor]]:
         """One epoch of (q, d) [batch, T] int32 device tensors. With world > 1 every rank
         takes its own contiguous slice of each global batch of batch*world pairs (the DP
-        sharding of train steps); one pinned host buffer and one async copy per tensor."""
+        sharding of train steps); the ranks' collectives need equal slices, so a ragged
+        last global batch is always dropped there. Two pinned host buffers alternate: the
+        host fills one while the other's async copy is in flight, and it only waits for
+        the copy event of the buffer it is about to overwrite (never for the step)."""
         n = len(self)
         order = np.random.default_rng(seed).permutation(n) if shuffle else np.arange(n)
         gb = batch * world
-        stop = (n // gb) * gb if drop_last else n
+        stop = (n // gb) * gb if (drop_last or world > 1) else n
         T = self.q.shape[1]
-        pin = torch.cuda.is_available() and torch.device(device).type == "cuda"
-        hq = torch.empty(batch, T, dtype=torch.int32, pin_memory=pin)
-        hd = torch.empty(batch, T, dtype=torch.int32, pin_memory=pin)
-        for g0 in range(0, stop, gb):
+        dev = torch.device(device)
+        pin = torch.cuda.is_available() and dev.type == "cuda"
+        bufs = [(torch.empty(batch, T, dtype=torch.int32, pin_memory=pin),
+                 torch.empty(batch, T, dtype=torch.int32, pin_memory=pin)) for _ in range(2)]
+        done = [None, None]  # copy-completion event of each host buffer pair
+        for i, g0 in enumerate(range(0, stop, gb)):
             sel = np.sort(order[g0 + rank * batch: min(g0 + (rank + 1) * batch, stop)])
             if len(sel) == 0:
                 break
             k = len(sel)
+            hq, hd = bufs[i & 1]
+            if done[i & 1] is not None:
+                done[i & 1].synchronize()  # the copy that last read this pair has finished
             hq[:k].numpy()[:] = self.q[sel]
             hd[:k].numpy()[:] = self.d[sel]
-            q = hq[:k].to(device, non_blocking=pin)
-            d = hd[:k].to(device, non_blocking=pin)
-            if pin:
-                torch.cuda.current_stream(torch.device(device)).synchronize()  # host buffers are reused
+            if dev.type == "cpu":  # a host target would alias the reused buffers
+                q, d = hq[:k].clone(), hd[:k].clone()
+            else:
+                q = hq[:k].to(dev, non_blocking=pin)
+                d = hd[:k].to(dev, non_blocking=pin)
+            if pin and dev.type == "cuda":
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(dev))
+                done[i & 1] = ev
             yield q, d
 
 

@@ -97,6 +97,22 @@ class _Packed:
         self.b2 = hd["3.bias"].float().contiguous()
 
 
+def _packed(p, cfg: TowerCfg, Ep: int, cache_ok: bool) -> _Packed:
+    """_Packed of one tower's parameters; for inference calls, cached on the first
+    parameter and reused while every parameter keeps its autograd version and storage
+    (optimizer steps and load_state_dict bump the version; two_towers_amd.Adam bumps it
+    explicitly). Writes through `.data` bypass version tracking, as for autograd itself."""
+    if not cache_ok:
+        return _Packed(p, cfg, Ep)
+    key = (cfg.dtype, cfg.H, cfg.head, Ep, tuple(t._version for t in p), tuple(t.data_ptr() for t in p))
+    hit = getattr(p[0], "_tt_pack", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    pk = _Packed(p, cfg, Ep)
+    p[0]._tt_pack = (key, pk)
+    return pk
+
+
 def _alloc(shape, dt, dev):
     return torch.empty(shape, dtype=dt, device=dev)
 
@@ -248,7 +264,7 @@ class TowersFn(torch.autograd.Function):
     (cfg.head "none": margin_two_tower.py:59-61, the head runs outside)."""
 
     @staticmethod
-    def forward(ctx, cfg: TowerCfg, table, group, *args):
+    def forward(ctx, cfg: TowerCfg, table, group, cache_ok, *args):
         n = cfg.ntowers
         xs, params = args[:n], args[n:]
         _lib.require_gpu(*xs, *params)
@@ -260,7 +276,7 @@ class TowersFn(torch.autograd.Function):
                 raise ValueError("query and doc inputs must share [B, T] in one fused call")
         Ep = ops.pad_cols(E, dt)
         npt = cfg.nparams
-        packs = [_Packed(params[i * npt:(i + 1) * npt], cfg, Ep) for i in range(n)]
+        packs = [_packed(params[i * npt:(i + 1) * npt], cfg, Ep, cache_ok) for i in range(n)]
         X0 = [featurize(x, table, Ep, dt) for x in xs]
         train_drop = cfg.drop_p > 0.0
         seeds = [int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) for _ in range(n)] if train_drop else [0] * n
@@ -385,7 +401,7 @@ class TowersFn(torch.autograd.Function):
         ctx.acts = None
         ctx.packs = None
         ctx.params = None
-        return (None, None, None, *([None] * n), *grads)
+        return (None, None, None, None, *([None] * n), *grads)
 
 
 def _layer_grads(gl, layer, E, Ep, dWih, dWhh, dbih, dbhh):
@@ -419,4 +435,7 @@ def run_towers(cfg: TowerCfg, table, xs, params, reduce_group=None, reduce: bool
         raise ValueError(f"GRU hidden size {cfg.H} must be a multiple of 8 on the HIP path "
                          "(the step epilogues update 8 consecutive units per thread)")
     group = (reduce_group,) if reduce and dist.active(reduce_group) else None
-    return TowersFn.apply(cfg, table, group, *xs, *params)
+    # inference (no gradient wanted): the packed compute copies may be reused while the
+    # parameters are unchanged (retrieval / serving encode many batches per weight version)
+    cache_ok = not (torch.is_grad_enabled() and any(p.requires_grad for p in params))
+    return TowersFn.apply(cfg, table, group, cache_ok, *xs, *params)

@@ -3,8 +3,9 @@
 BASELINE configs[2] runs EnhancedTwoTowerModel(300, 256) (GRU H = 512 per direction),
 seq_len 64, bf16, dropout 0.1, hard-negative mining k = 5 + MarginRankingLoss(0.2).
 These tests run exactly the kernels that step runs -- the persistent bf16 GRU forward
-(gru_fwd_seq<4, 8>), the 256x256 BPTT step kernel (gru_bwd_big), the persistent
-input-projection GEMMs, the fp32 head -- at a batch the oracle finishes in seconds, and
+(gru_fwd_seq<4, 8>), the row-owning BPTT kernel (gru_bwd_rows<512>, one launch per
+layer), the persistent input-projection GEMMs, the fp32 head, the hard-negative scan --
+at a batch the oracle finishes in seconds, and
 compare with oracle/cpu_ref.py (reference enhanced_two_tower.py:50-65, :67-82, :84-133)
 evaluated in fp32 on the same bf16-rounded weights and inputs, so only the kernels'
 internal bf16 rounding (operands of every MFMA, the saved pre-activations, the bf16

@@ -58,3 +58,43 @@ def test_pretokenized_training_and_search(tmp_path, family):
     assert [r["rank"] for r in res["results"]] == [1, 2, 3]
     scores = [r["score"] for r in res["results"]]
     assert scores == sorted(scores, reverse=True) and -1.0001 <= scores[-1] <= scores[0] <= 1.0001
+
+
+def test_bin_store_ids_and_device_gather_match_reference_featurization(tmp_path):
+    """The whole data path pinned to the reference's own featurisation (featurize.npz,
+    EnhancedDataset.text_to_embedding run by oracle/gen_goldens.py, and margin_featurize.npz,
+    SimpleDataset): the fixture's word vectors written as word2vec.c binary bytes (header
+    "V E\\n", then "word " + E little-endian float32 + "\\n" per row), read back, saved as the
+    flat store, the texts pre-tokenized into id files, and the ids gathered on the GPU by
+    tt_embed_gather through the model's table: every [T, E] row equals the reference's,
+    bit for bit (fp32)."""
+    import os
+
+    from two_towers_amd import ops
+    gold = os.path.join(os.path.dirname(__file__), "golden")
+    for fixture, tok in (("featurize", "enhanced"), ("margin_featurize", "margin")):
+        z = np.load(os.path.join(gold, fixture + ".npz"), allow_pickle=False)
+        words, vecs = [str(w) for w in z["words"]], z["vecs"].astype(np.float32)
+        V, E = vecs.shape
+        path = tmp_path / f"{tok}.bin"
+        with open(path, "wb") as f:
+            f.write(f"{V} {E}\n".encode())
+            for w, v in zip(words, vecs):
+                f.write(w.encode("utf-8") + b" " + struct.pack(f"<{E}f", *v) + b"\n")
+        vocab = w2v.read_word2vec_format(str(path))
+        assert [w for w, _ in sorted(vocab.index.items(), key=lambda kv: kv[1])] == words
+        assert np.array_equal(vocab.vectors, vecs)
+        w2v.save_store(vocab, str(tmp_path / f"store_{tok}"))
+        store = w2v.load_store(str(tmp_path / f"store_{tok}"))
+        texts = [str(t) for t in z["texts"]]
+        T = int(z["max_length"])
+        pretok.pretokenize(texts, texts, store, str(tmp_path / f"ids_{tok}"), T, tok, workers=1)
+        ds = pretok.PairIds(str(tmp_path / f"ids_{tok}"), store)
+        ids = torch.stack([ds[i][0] for i in range(len(ds))]).cuda()
+        m = EnhancedTwoTowerModel(E, 4).cuda()
+        m.set_embedding_table(torch.from_numpy(np.array(store.vectors)).cuda())
+        tab = m._device_table(ids.device)
+        out = torch.empty(ids.numel(), tab.shape[1], device="cuda")
+        ops.embed_gather(tab, ids.reshape(-1).to(torch.int32).contiguous(), out)
+        got = out[:, :E].reshape(len(texts), T, E).cpu().numpy()
+        np.testing.assert_array_equal(got, z["emb"])

@@ -78,12 +78,14 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--ops", default="hardneg,infonce")
+    ap.add_argument("--hn-shapes", default="8192x8192x256,8192x65536x256,8192x8192x512",
+                    help="hard-negative shapes B x N x h")
     a = ap.parse_args()
     bf = torch.bfloat16
     if "hardneg" in a.ops:
-        for B, nd in ((8192, 8192), (8192, 65536)):
-            print(json.dumps(hardneg(B, nd, 256, 5, bf, a.iters)), flush=True)
-        print(json.dumps(hardneg(8192, 8192, 512, 5, bf, a.iters)), flush=True)
+        for shp in a.hn_shapes.split(","):
+            B, nd, h = (int(x) for x in shp.split("x"))
+            print(json.dumps(hardneg(B, nd, h, 5, bf, a.iters)), flush=True)
     if "infonce" in a.ops:
         for B, nd, h in ((8192, 8192, 256), (8192, 65536, 256), (8192, 8192, 512)):
             print(json.dumps(infonce(B, nd, h, bf, a.iters)), flush=True)

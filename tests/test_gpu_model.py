@@ -290,3 +290,29 @@ def test_packed_weight_cache_follows_parameter_versions():
     with torch.no_grad():
         d = m.encode_query(x)
     assert torch.equal(d, fresh_out())
+
+
+@pytest.mark.parametrize("h,B,T,dt", [(512, 300, 3, torch.bfloat16), (48, 520, 4, torch.float32)])
+def test_per_step_forward_256_row_tiles(h, B, T, dt):
+    """Per-step GRU forward (the path of H > 512 in bf16, e.g. configs[4]'s H = 1024, and of
+    fp32) on 256-row tiles (8 waves) vs 128-row tiles (option gru_fwd_step_rows): the same
+    K order per output, so outputs and gradients agree to fp32 rounding. B 300 / 520 give
+    tail row tiles."""
+    E = 40
+    g = torch.Generator().manual_seed(15)
+    q = torch.randn(B, T, E, generator=g).to(DEV)
+    d = torch.randn(B, T, E, generator=g).to(DEV)
+    outs = []
+    for rows in (128, 256):
+        m, _ = make_model(E, h, 3)
+        m = m.to(DEV).train().set_compute_dtype(dt)
+        with option("gru_step", 1), option("gru_fwd_step_rows", rows):
+            qv, dv = m(q, d)
+            loss = tta.InfoNCELoss(compute_dtype=dt)(qv, dv)
+            loss.backward()
+        outs.append((qv.detach().clone(), dv.detach().clone(), {k: p.grad.clone() for k, p in m.named_parameters()}))
+    q0, d0, g0 = outs[0]
+    for q1, d1, g1 in outs[1:]:
+        assert rel(q1, q0) < 1e-5 and rel(d1, d0) < 1e-5
+        for k in g0:
+            assert rel(g1[k], g0[k]) < 1e-4, k

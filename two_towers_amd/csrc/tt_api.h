@@ -26,6 +26,7 @@ enum Opt {
   OPT_GRU_BWD_PERSIST,  // 0: per-step backward launches instead of the row-owning kernel
   OPT_GRU_BWD_R64,      // 1: row-owning backward with 64-row workgroups, two per CU
   OPT_GRU_BWD_PHASE,    // gru_bwd_r64: start delay of the grid's second half (s_sleep 127 units)
+  OPT_GRU_FWD_STEP_ROWS, // per-step GRU forward batch rows per tile: 128, 256 (0: by size)
   OPT_INFONCE_FLASH,    // 0: InfoNCE backward through a materialised dS (bf16, h 128/256 default fused)
   OPT_N
 };

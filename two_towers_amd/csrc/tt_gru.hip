@@ -62,18 +62,23 @@ struct GateRows {
   TT_DEV const T* at(int r, int k) const { const T* p = rowptr(r); return p ? p + k : nullptr; }
 };
 
-template <typename T>
-__global__ __launch_bounds__(256) void gru_fwd_step(FwdArgs a) {
-  using ML = ttg::DLoop<T, false, false, 128, 192, 2, 2>;
+// BMR batch rows per tile: 128 (4 waves, two workgroups per CU) or 256 (8 waves as 4 x 2,
+// half the W_hh traffic per FLOP and twice the MFMA work per K-tile barrier): at configs[4]
+// (H 1024, B 8192) 48.0-48.6 vs 50.3-51.5 ms per layer. A 4-stage LDS ring with counted
+// waits on 128-row tiles (one workgroup per CU) measured 85.7 ms.
+template <typename T, int BMR>
+__global__ __launch_bounds__(2 * BMR) void gru_fwd_step(FwdArgs a) {
+  constexpr int NT = 2 * BMR;
+  using ML = ttg::DLoop<T, false, false, BMR, 192, BMR / 64, 2>;
   __shared__ __attribute__((aligned(16))) char lds[ML::LDS_BYTES];
   // 1-D grid, XCD-aware: the H/64 unit tiles of one batch tile are consecutive ids on one
   // XCD, so its h_{s-1} panel is fetched into that XCD's L2 once, not once per tile.
-  const int ntj = (a.H + 63) / 64, ntm = (a.B + 127) / 128;
+  const int ntj = (a.H + 63) / 64, ntm = (a.B + BMR - 1) / BMR;
   const int id = ttg::xcd_remap(blockIdx.x, gridDim.x);
   const int rz = id / (ntm * ntj), rem = id - rz * ntm * ntj;
   const FwdRec R = a.r[rz];
   const int H = a.H, T_ = a.T, s = a.s;
-  const int m0 = (rem / ntj) * 128, j0 = (rem % ntj) * 64;
+  const int m0 = (rem / ntj) * BMR, j0 = (rem % ntj) * 64;
   const int t = R.dir ? T_ - 1 - s : s;
   const int tp = R.dir ? t + 1 : t - 1;
   const T* Y = static_cast<const T*>(R.y);
@@ -104,7 +109,7 @@ __global__ __launch_bounds__(256) void gru_fwd_step(FwdArgs a) {
   const float* hs_prv = R.hs + (long)prv * a.B * H;
   const __amdgpu_buffer_rsrc_t srs = tt_rsrc(S + ((long)m0 * T_ + t) * (4L * H));
   const __amdgpu_buffer_rsrc_t xrs = tt_rsrc(X1 ? X1 + ((long)m0 * T_ + t) * a.ldy : Yw);
-  for (int hf = 0; hf < 2; ++hf) {
+  for (int hf = 0; hf < BMR / 64; ++hf) {
     if ((wave >> 1) == hf) {
       const int nb = (wave & 1) * 32;
 #pragma unroll
@@ -119,8 +124,8 @@ __global__ __launch_bounds__(256) void gru_fwd_step(FwdArgs a) {
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int rl = (tid >> 3) + 32 * k, jg = (tid & 7) * 8;
+    for (int k = 0; k < 512 / NT; ++k) {
+      const int rl = (tid >> 3) + (NT / 8) * k, jg = (tid & 7) * 8;
       const int b = m0 + hf * 64 + rl, j = j0 + jg;
       if (b < a.B && j < H) {
         const long row = (long)b * T_ + t;
@@ -1384,11 +1389,21 @@ extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B
     TT_CHECK_LAUNCH("gru_fwd_seq");
     return 0;
   }
-  dim3 grid(tt_ceil_div(H, 64) * tt_ceil_div(B, 128) * nrec);
+  // 256-row tiles where they still give >= 2 workgroups per CU (option gru_fwd_step_rows
+  // 128 / 256 forces one)
+  int bmr = tt::opt(tt::OPT_GRU_FWD_STEP_ROWS);
+  if (bmr != 128 && bmr != 256)
+    bmr = (long)tt_ceil_div(H, 64) * tt_ceil_div(B, 256) * nrec >= 512 ? 256 : 128;
+  dim3 grid(tt_ceil_div(H, 64) * tt_ceil_div(B, bmr) * nrec);
   for (int s = 0; s < T; ++s) {
     a.s = s;
-    if (dtype == TT_DT_BF16) hipLaunchKernelGGL(gru_fwd_step<bf16_t>, grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(gru_fwd_step<float>, grid, dim3(256), 0, st, a);
+    if (dtype == TT_DT_BF16) {
+      if (bmr == 256) hipLaunchKernelGGL((gru_fwd_step<bf16_t, 256>), grid, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((gru_fwd_step<bf16_t, 128>), grid, dim3(256), 0, st, a);
+    } else {
+      if (bmr == 256) hipLaunchKernelGGL((gru_fwd_step<float, 256>), grid, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((gru_fwd_step<float, 128>), grid, dim3(256), 0, st, a);
+    }
     TT_CHECK_LAUNCH("gru_fwd_step");
   }
   return 0;

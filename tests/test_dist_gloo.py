@@ -55,7 +55,7 @@ def _worker(rank, world, port, q, d, p0, out):
     torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4])
 def test_dp_gather_loss_and_grads_match_single_process(world):
     torch.manual_seed(0)
     p0 = cpu_ref.counter_params(12, 8, 3)

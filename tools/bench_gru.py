@@ -88,7 +88,9 @@ def main():
         set_option("gru_bwd_persist", 1 if rows in ("P", "R") else 0)
         set_option("gru_bwd_r64", 1 if rows == "R" else 0)
         set_option("gru_bwd_phase", int(dbg) if rows == "R" else 0)
-        set_option("gru_bwd_rows", 128 if rows in ("P", "R") else int(rows))
+        # S: the 128x128 per-step kernels (gru_bwd_big = 0) with `strm` stream chains
+        set_option("gru_bwd_big", 0 if rows == "S" else 1)
+        set_option("gru_bwd_rows", 128 if rows in ("P", "R", "S") else int(rows))
         os.environ["TT_GRU_DBG"] = dbg  # read only by a -DTT_DIAG build
         set_option("gru_bwd_streams", int(strm))
         brecs, bkeep = setup_bwd(a.B, a.T, a.H, keep, dev)

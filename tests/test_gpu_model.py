@@ -316,3 +316,43 @@ def test_per_step_forward_256_row_tiles(h, B, T, dt):
         assert rel(q1, q0) < 1e-5 and rel(d1, d0) < 1e-5
         for k in g0:
             assert rel(g1[k], g0[k]) < 1e-4, k
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,T", [(1, 1), (1, 30), (2, 1), (3, 64)])
+def test_tiny_batches_and_sequences(B, T, dt):
+    """Edge shapes of the drop-in surface: validate_enhanced.py:61-71 encodes ONE text at a
+    time ([1, T, E]), T = 1 has no recurrent term past the first step, B = 2 / 3 leave
+    almost every row tile empty. encode_query / encode_doc and a train-mode InfoNCE
+    backward against the oracle (fp32: 1e-4 outputs, 2e-3 gradients; bf16: the operand
+    rounding of the bench-path tests, 3e-2 outputs)."""
+    E, h = 300, 64
+    m, p = make_model(E, h, 17)
+    m = m.to(DEV).set_compute_dtype(dt).eval()
+    g = torch.Generator().manual_seed(B * 100 + T)
+    q = torch.randn(B, T, E, generator=g) * 0.5
+    d = torch.randn(B, T, E, generator=g) * 0.5
+    if dt == torch.bfloat16:
+        q, d = q.to(dt).float(), d.to(dt).float()
+        p = {k: v.to(dt).float() for k, v in p.items()}
+        m.load_state_dict(p)
+    tol = 1e-4 if dt == torch.float32 else 3e-2
+    with torch.no_grad():
+        eq = m.encode_query(q.to(DEV))
+        ed = m.encode_doc(d.to(DEV))
+    assert eq.shape == (B, h) and ed.shape == (B, h)
+    assert rel(eq, cpu_ref.encode(q, p, "query")) < tol and rel(ed, cpu_ref.encode(d, p, "doc")) < tol
+    if B < 2:
+        return
+    qv, dv = m(q.to(DEV), d.to(DEV))
+    loss = tta.InfoNCELoss(compute_dtype=dt)(qv, dv)
+    loss.backward()
+    pr = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    rl = cpu_ref.infonce(*cpu_ref.forward(q, d, pr))
+    rl.backward()
+    lv, rv = float(loss.detach()), float(rl.detach())
+    assert abs(lv - rv) < (1e-4 if dt == torch.float32 else 2e-2) * max(1.0, abs(rv))
+    if dt == torch.float32:
+        named = dict(m.named_parameters())
+        worst = max(rel(named[k].grad, pr[k].grad) for k in pr)
+        assert worst < 2e-3, worst

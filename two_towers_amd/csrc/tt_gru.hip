@@ -519,33 +519,53 @@ __global__ __launch_bounds__(512) void gru_bwd_big(BwdArgs a) {
 // ---- persistent ("row-owning") backward, bf16, H in {256, 512} --------------------
 // One launch per layer. A workgroup (8 waves) owns 128 batch rows x ALL H units of one
 // recurrence and walks every time step itself: batch rows never interact, so no step
-// waits for another workgroup, and workgroups drift out of phase -- one CU's HBM-bound
-// epilogue streams while another's recurrent GEMM runs, instead of every CU doing the
-// GEMM (HBM idle) and then the epilogue (MFMA idle) in lockstep, once per launch.
+// waits for another workgroup.
 // Per step: acc[128 x H] = dL/dgh_{s+1}[128 x 3H] . W_hh[3H x H] on MFMA (A: the rows'
 // own gradients of the previous iteration, K-contig, r|z from dgx and n from dgh; B: W_hh,
 // K-outer, read from the XCD's L2), then the gate gradients with the accumulator tile
-// staged through the freed LDS; the step's bias partials are added into the tile's
-// partial row.
-//   LDS: 2 slots x (A 16 KiB + H/128 B sub-images of 16 KiB) = 160 KiB at H = 512; the
-//   epilogue's bf16 [128][H] accumulator image reuses them.
-// Waves as 2 (rows) x 4 (columns): wave tile 64 x H/4, acc[4][H/64] of 16x16 MFMA tiles.
+// staged once as a bf16 image through the freed LDS; the step's bias partials are added
+// into the tile's partial row. The product runs on 32-deep K-tiles (A 128 rows x 64 B =
+// 8 KiB, W_hh 32 k x H = H/128 sub-images of 8 KiB) in a 4-slot LDS ring with three
+// K-tiles in flight and counted waits (vmcnt = this wave's DMAs of the younger tiles):
+// 7.61 vs 7.81 ms per layer at configs[2] against 64-deep K-tiles in two slots.
+//   A image: 64-byte rows, 16-byte chunk c of row r at c ^ ((r >> 1) & 3) (conflict-free
+//   for the ds_read_b128 lane groups); W_hh: the K-outer bf16 image of the first 32 k-rows.
 template <int H>
 struct BwdRowsCfg {
-  static constexpr int NQ = H / 128;             // B sub-images per K-tile
-  static constexpr int SLOT = (1 + NQ) * 16384;  // one K-tile: A + B
-  static constexpr int LDS = 2 * SLOT;
-  static constexpr int NCB = H / 64;             // 16-column blocks per wave
-  static constexpr int TPR = H / 8;              // epilogue threads per row (8 units each)
-  static constexpr int RPI = 512 / TPR;          // rows per epilogue iteration
-  static constexpr int LDB = H + 8;              // staged bf16 row pitch (bank spread)
-  static_assert(128 * LDB * 2 <= LDS && RPI * 4 * H * 4 <= LDS, "staging fits the slots");
+  static constexpr int NQ = H / 128;
+  static constexpr int SLOT = 8192 + NQ * 8192;  // 40 KiB at H = 512
+  static constexpr int NS = 4;
+  static constexpr int LDS = NS * SLOT;
+  static constexpr int P = SLOT / 1024 / 8;  // DMAs per wave per K-tile
+  static constexpr int NCB = H / 64;
+  static constexpr int TPR = H / 8;
+  static constexpr int RPI = 512 / TPR;
+  static constexpr int LDB = H + 8;
+  static_assert(SLOT % 8192 == 0 && 128 * LDB * 2 <= LDS && RPI * 4 * H * 4 <= LDS, "ring layout");
 };
+
+TT_DEV uint4 frag_kc64(const char* img, int r0) {  // A fragment of a 32-deep, 64-byte-row image
+  const int lane = threadIdx.x & 63;
+  const int row = r0 + (lane & 15);
+  return *reinterpret_cast<const uint4*>(img + row * 64 + (((lane >> 4) ^ ((row >> 1) & 3)) << 4));
+}
+
+template <int N, int P>
+TT_DEV void wait_younger(int n) {  // s_waitcnt vmcnt(P * n), n in [0, N]
+  if constexpr (N > 0) {
+    if (n >= N) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P * N) : "memory");
+      return;
+    }
+    wait_younger<N - 1, P>(n);
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
 
 template <int H>
 __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
   using C = BwdRowsCfg<H>;
-  using L8 = ttg::Loop8<bf16_t, false, true>;
   __shared__ __attribute__((aligned(16))) char lds[C::LDS];
   const int T_ = a.T, ntm = (a.B + 127) / 128;
   const int id = ttg::xcd_remap(blockIdx.x, gridDim.x);
@@ -561,14 +581,31 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
   const bf16_t* S = static_cast<const bf16_t*>(R.save);
   const bf16_t* Y = static_cast<const bf16_t*>(R.y);
   const bf16_t* DY = static_cast<const bf16_t*>(R.dy);
+  const bf16_t* W = static_cast<const bf16_t*>(R.whh);
   const uint32_t lbase = __builtin_amdgcn_readfirstlane(ttg::lds_addr_of(lds));
-  constexpr int K = 3 * H, NK = K / L8::KTE;
-  const long dk = (long)L8::KTE * H * 2;  // bytes between K-tiles of the K-outer W_hh
-  const ttg::KOPlain<bf16_t> lb{static_cast<const bf16_t*>(R.whh), H, 0, H};
-  // epilogue ownership: units jg .. jg+7 of rows rsub + RPI i
+  constexpr int NK = 3 * H / 32;  // 32-deep K-tiles per step
+  const long ldr = (long)T_ * a.ldd;
+  // DMA pieces of a slot, wave + 8j (j < P): piece 0..7 = the A image (row q >> 2, chunk
+  // slot q & 3 of 16-byte unit q), then NQ x 8 pieces of W_hh sub-images (k-row q >> 4,
+  // chunk slot q & 15)
+  int prow[C::P], pcol[C::P];
+#pragma unroll
+  for (int j = 0; j < C::P; ++j) {
+    const int pc = wave + 8 * j, q = (pc & 7) * 64 + lane;
+    if (pc < 8) {
+      const int row = q >> 2;
+      prow[j] = row;
+      pcol[j] = ((q & 3) ^ ((row >> 1) & 3)) * 8;
+    } else {
+      const int sub = (pc - 8) >> 3, kl = q >> 4;
+      prow[j] = -1;
+      pcol[j] = kl * H + sub * 128 + (((q & 15) ^ (ttg::ko_v(kl) << 1)) * 8);
+    }
+  }
   const int jg = (tid % C::TPR) * 8, rsub = tid / C::TPR;
   float* L = reinterpret_cast<float*>(lds);
-  float* part = R.dbias + (long)mt * (4L * H);  // this tile's partial row (zeroed by the host)
+  float* part = R.dbias + (long)mt * (4L * H);
+  const char* zp = reinterpret_cast<const char*>(ttg::g_tt_zero_page);
 #ifdef TT_DIAG
   const int dbg = a.dbg;  // diagnostic build only: 1 no GEMM, 2 no epilogue loads, 4 no stores
 #else
@@ -586,68 +623,64 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
 #pragma unroll
       for (int j = 0; j < C::NCB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (!last && !(dbg & 1)) {
-      // A = dL/dgh_{s+1} of this workgroup's rows, written by its own previous iteration
-      const ttg::KCSplit<bf16_t> la{DGX + (long)tn * a.ldd, DGH + (long)tn * a.ldd, (long)T_ * a.ldd, m0, a.B, 2 * H};
-      // B pieces: sub-image q is the same pattern 128 columns (256 B) further right, and
-      // W_hh is fully in range, so one piece per DMA slot serves all q
-      typename L8::Piece pa[2], pb[2];
-      L8::template init_half<false>(la, 0, NK, K, 0, pa);
-      L8::template init_half<true>(lb, 0, NK, K, 0, pb);
-      auto issue_b = [&](int r, uint32_t img) {
+      // A source of this lane's A pieces: dL/dgh_{s+1} of row m0 + prow, r|z from dgx, n from dgh
+      const char* as0[C::P];
+      const char* as1[C::P];
+#pragma unroll
+      for (int j = 0; j < C::P; ++j) {
+        const int b = m0 + (prow[j] < 0 ? 0 : prow[j]);
+        const bool ok = prow[j] >= 0 && b < a.B;
+        as0[j] = ok ? reinterpret_cast<const char*>(DGX + (long)tn * a.ldd + (long)b * ldr + pcol[j]) : zp;
+        as1[j] = ok ? reinterpret_cast<const char*>(DGH + (long)tn * a.ldd + (long)b * ldr + pcol[j] - 2 * H) : zp;
+      }
+      auto issue = [&](int r) {
+        const uint32_t img = lbase + (uint32_t)(r % C::NS) * C::SLOT;
         const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const bool hi = r * 32 >= 2 * H;
 #pragma unroll
-        for (int q = 0; q < C::NQ; ++q)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            ttg::dma16(pb[j].p + (long)r * dk + 256 * q, img + 16384u * (1 + q) + (uint32_t)(wv + 8 * j) * 1024u);
-      };
-      L8::issue_half(la, pa, 0, (long)ttg::KTB, lbase);
-      issue_b(0, lbase);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      for (int r = 0; r < NK; ++r) {
-        const int cs = r & 1;
-        const char* sl = lds + cs * C::SLOT;
-        if (r + 1 < NK) {  // K-tile r+1 flies during K-tile r's MFMAs; its slot was freed by
-                           // the barrier that ended K-tile r-1
-          const uint32_t nx = lbase + (cs ^ 1) * C::SLOT;
-          L8::issue_half(la, pa, r + 1, (long)ttg::KTB, nx);
-          issue_b(r + 1, nx);
+        for (int j = 0; j < C::P; ++j) {
+          const int pc = wv + 8 * j;
+          const char* src;
+          if (pc < 8) {
+            src = hi ? as1[j] : as0[j];
+            if (src != zp) src += (long)r * 64;  // 32 k of bf16
+          } else {
+            src = reinterpret_cast<const char*>(W + (long)r * 32 * H + pcol[j]);
+          }
+          ttg::dma16(src, img + (uint32_t)pc * 1024u);
         }
-        uint4 fa[2][4];
+      };
+      issue(0);
+      issue(1);
+      issue(2);
+#pragma unroll 1
+      for (int r = 0; r < NK; ++r) {
+        wait_younger<C::NS - 2, C::P>(NK - 1 - r);  // tile r landed (up to 2 younger in flight)
+        __builtin_amdgcn_s_barrier();               // everyone's; slot (r + 3) % 4 = r - 1's is free
+        if (r + 3 < NK) issue(r + 3);
+        const char* sl = lds + (r % C::NS) * C::SLOT;
+        uint4 fa[4];
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) fa[ks][i] = ttg::frag<bf16_t, false>(sl, wr * 64 + 16 * i, ks);
-        const char* ib = sl + 16384 + ((wc * (H / 4)) >> 7) * 16384;
+        for (int i = 0; i < 4; ++i) fa[i] = frag_kc64(sl, wr * 64 + 16 * i);
+        const char* ib = sl + 8192 + ((wc * (H / 4)) >> 7) * 8192;
         const int cb = (wc * (H / 4)) & 127;
 #pragma unroll
         for (int jp = 0; jp < C::NCB; jp += 2) {
-          uint4 fb[2][2];
+          uint4 fb[2];
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) fb[ks][j] = ttg::frag<bf16_t, true>(ib, cb + 16 * (jp + j), ks);
+          for (int j = 0; j < 2; ++j) fb[j] = ttg::frag<bf16_t, true>(ib, cb + 16 * (jp + j), 0);
           __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks)
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-              for (int j = 0; j < 2; ++j) acc[i][jp + j] = ttg::mma<bf16_t>(fa[ks][i], fb[ks][j], acc[i][jp + j]);
+            for (int j = 0; j < 2; ++j) acc[i][jp + j] = ttg::mma<bf16_t>(fa[i], fb[j], acc[i][jp + j]);
           __builtin_amdgcn_s_setprio(0);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of K-tile r+1
-        __builtin_amdgcn_s_barrier();                      // everyone's; slot cs is free
       }
+      __builtin_amdgcn_s_barrier();  // every wave done with the slots before the staging
     }
-    // ---- epilogue: the whole 128 x H accumulator tile is staged at once as a bf16 image
-    // [128][LDB] over the freed slots (the recurrent term rounded to bf16 like the carry
-    // and the GEMM operands it is summed with), so every accumulator register is free
-    // before the gate arithmetic and the rows' loads can be batched NB deep.
+    // ---- epilogue: as gru_bwd_rows
     const long trow = (long)m0 * T_ + t;
-    // carry dh*z in bf16: an fp32 carry measured the same gradient error vs the fp32
-    // oracle (tools/diag_bench_path.py) at 10 % more time
     const __amdgpu_buffer_rsrc_t rc =
         tt_rsrc_n(static_cast<const bf16_t*>(R.dh) + (long)((s + 1) & 1) * a.B * H + (long)m0 * H, !last);
     bf16_t* cr_cur = static_cast<bf16_t*>(R.dh) + (long)(s & 1) * a.B * H + (long)m0 * H;
@@ -655,7 +688,7 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
     const __amdgpu_buffer_rsrc_t rsv = tt_rsrc_n(S + trow * 4L * H, true);
     const __amdgpu_buffer_rsrc_t ry = tt_rsrc_n(s > 0 ? Y + ((long)m0 * T_ + tp) * a.ldy : S, s > 0);
     const __amdgpu_buffer_rsrc_t grs = tt_rsrc(DGXw + trow * a.ldd);
-    uint32_t* L16 = reinterpret_cast<uint32_t*>(lds);  // bf16 image, row pitch LDB elements
+    uint32_t* L16 = reinterpret_cast<uint32_t*>(lds);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -670,13 +703,13 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int e = 0; e < 8; ++e) bsum[q][e] = 0.f;
-    constexpr int NB = 2;  // rows per load batch: 2 x 7 loads of 16 B in flight per thread
+    constexpr int NB = 2;
 #pragma unroll 1
     for (int kb = 0; kb < 128 / C::RPI; kb += NB) {
       uint4 vin[NB][7];
 #pragma unroll
       for (int kk = 0; kk < NB; ++kk) {
-        const int bl = rsub + C::RPI * (kb + kk);  // row within the tile
+        const int bl = rsub + C::RPI * (kb + kk);
         const bool ok = m0 + bl < a.B && !(dbg & 2);
         const uint32_t oc = ok ? (uint32_t)(bl * H + jg) * 2u : 0x80000000u;
         const uint32_t oy = ok ? (uint32_t)(bl * T_ * (int)a.ldy + jg) * 2u : 0x80000000u;
@@ -701,7 +734,7 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
         unpack8(vin[kk][5], gh);
         unpack8(vin[kk][6], hp);
         unpack8(*reinterpret_cast<const uint4*>(L16 + ((bl * C::LDB + jg) >> 1)), gm);
-        if (last && R.dfinal) ld8(R.dfinal + (long)b * a.ldf + jg, cin);  // fp32 final-state gradient
+        if (last && R.dfinal) ld8(R.dfinal + (long)b * a.ldf + jg, cin);
         float o_r[8], o_z[8], o_n[8], o_hn[8], cout[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -730,10 +763,8 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
         st8(DGHw + row * a.ldd + jg, o_hn);
       }
     }
-    __syncthreads();  // the image is rewritten by the bias reduction
-    // the step's bias partials: the RPI threads sharing each unit group meet in LDS, then
-    // one add per column into the tile's partial row (owned by this workgroup alone)
-    float* red = L;  // [RPI][4][H]
+    __syncthreads();
+    float* red = L;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -745,8 +776,6 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
       for (int w = 0; w < C::RPI; ++w) v += red[w * 4 * H + c];
       part[c] += v;
     }
-    // this step's dL/dgh and carry are the next iteration's operands: every wave's stores
-    // must have reached L2 before any wave issues the DMA that reads them
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }

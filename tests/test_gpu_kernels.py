@@ -126,14 +126,18 @@ def test_adam_matches_torch():
         assert torch.allclose(a.detach(), b.detach().cpu(), rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("akout,bkout", [(0, 0), (0, 1), (1, 1)])
+@pytest.mark.parametrize("akout,bkout", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("out", [torch.bfloat16, torch.float32])
-def test_gemm_persistent_tiles(akout, bkout, out):
+@pytest.mark.parametrize("n", [4104, 4100])
+def test_gemm_persistent_tiles(akout, bkout, out, n):
     """Shapes with >= 512 256x256 tiles and a short K run the persistent kernel (K-tile
     stream across tiles): ragged M/N/K tails, bias, relu, two batch entries; compared
-    with fp32 math on the same bf16-rounded operands."""
+    with fp32 math on the same bf16-rounded operands; n = 4100 leaves rows that are not
+    16-byte aligned (element stores)."""
+    if bkout and n % 8:
+        pytest.skip("a K-outer B needs 16-byte rows (ldb = n)")
     dt = torch.bfloat16
-    m, n, k = 8200, 4104, 136
+    m, k = 8200, 136
     g = torch.Generator().manual_seed(5)
     As = [torch.randn(m, k, generator=g).to(dt).float() for _ in range(2)]
     Bs = [torch.randn(n, k, generator=g).to(dt).float() for _ in range(2)]

@@ -16,18 +16,25 @@ SHAPES = {  # name: (m, n, k, a_kouter, b_kouter, nbatch, out_bf16)
     "wgrad_ih1": (1536, 1024, 524288, 1, 1, 4, 0),
     "wgrad_hh": (1536, 512, 524288, 1, 1, 4, 0),
     "square8k": (8192, 8192, 8192, 0, 0, 1, 1),
+    # diagnostics: K padded to whole 128-B lines; the l1 FLOPs with a B small enough for L2
+    "input_proj_l0_k320": (524288, 3072, 320, 0, 0, 2, 1),
+    "proj_l1_n768": (2097152, 768, 1024, 0, 0, 2, 1),
+    "sq_k1024": (16384, 16384, 1024, 0, 0, 1, 1),
 }
 
 
-def run(name, iters):
+def run(name, iters, lda_pad=0):
     m, n, k, ak, bk, nb, obf = SHAPES[name]
     dt = torch.bfloat16
-    A = [torch.randn((k, m) if ak else (m, k), device="cuda").to(dt) for _ in range(nb)]
+    if lda_pad and not ak:  # A rows lda_pad elements apart (a strided view)
+        A = [torch.randn(m, lda_pad, device="cuda").to(dt)[:, :k] for _ in range(nb)]
+    else:
+        A = [torch.randn((k, m) if ak else (m, k), device="cuda").to(dt) for _ in range(nb)]
     B = [torch.randn((k, n) if bk else (n, k), device="cuda").to(dt) for _ in range(nb)]
     odt = dt if obf else torch.float32
     C = [torch.empty(m, n, device="cuda", dtype=odt) for _ in range(nb)]
     bias = [torch.randn(n, device="cuda") for _ in range(nb)] if obf else None
-    f = lambda: ops.gemm(A, B, C, m=m, n=n, k=k, lda=m if ak else k, ldb=n if bk else k, ldc=n, a_kouter=bool(ak),
+    f = lambda: ops.gemm(A, B, C, m=m, n=n, k=k, lda=m if ak else (lda_pad or k), ldb=n if bk else k, ldc=n, a_kouter=bool(ak),
                          b_kouter=bool(bk), dtype=dt, out_dtype=odt, bias=bias)
     f()
     torch.cuda.synchronize()
@@ -47,8 +54,9 @@ if __name__ == "__main__":
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--regstage", default="", help="TT_GEMM_REGSTAGE value (9 = no epilogue, timing only)")
+    ap.add_argument("--lda-pad", type=int, default=0, help="A row stride in elements (K-contig A)")
     a = ap.parse_args()
     if a.regstage:
         os.environ["TT_GEMM_REGSTAGE"] = a.regstage
     for nm in a.shapes.split(","):
-        print(json.dumps(run(nm, a.iters)), flush=True)
+        print(json.dumps(run(nm, a.iters, a.lda_pad)), flush=True)

@@ -162,7 +162,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_kernel(GemmArgs g) {
 
 #ifdef TT_DIAG
   if (g.force_regstage == 9) {  // diagnostic build only: main loop without epilogue
-    if (threadIdx.x == 0 && acc[0][0][0] == 12345.f) static_cast<float*>(g.c[bi])[0] = 1.f;
+    float sum = 0.f;  // every accumulator chain stays live (no MFMA is dead code)
+#pragma unroll
+    for (int i = 0; i < ML::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < ML::TN; ++j) sum += acc[i][j][0] + acc[i][j][3];
+    if (sum == 12345.f) static_cast<float*>(g.c[bi])[0] = 1.f;
     return;
   }
 #endif

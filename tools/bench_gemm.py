@@ -26,7 +26,9 @@ SHAPES = {  # name: (m, n, k, a_kouter, b_kouter, nbatch, out_bf16)
 def run(name, iters, lda_pad=0):
     m, n, k, ak, bk, nb, obf = SHAPES[name]
     dt = torch.bfloat16
-    if lda_pad and not ak:  # A rows lda_pad elements apart (a strided view)
+    if lda_pad < 0 and not ak:  # every A row the same 16 KiB-or-less row (lda 0): A from L2
+        A = [torch.randn(1, k, device="cuda").to(dt) for _ in range(nb)]
+    elif lda_pad and not ak:  # A rows lda_pad elements apart (a strided view)
         A = [torch.randn(m, lda_pad, device="cuda").to(dt)[:, :k] for _ in range(nb)]
     else:
         A = [torch.randn((k, m) if ak else (m, k), device="cuda").to(dt) for _ in range(nb)]
@@ -34,7 +36,7 @@ def run(name, iters, lda_pad=0):
     odt = dt if obf else torch.float32
     C = [torch.empty(m, n, device="cuda", dtype=odt) for _ in range(nb)]
     bias = [torch.randn(n, device="cuda") for _ in range(nb)] if obf else None
-    f = lambda: ops.gemm(A, B, C, m=m, n=n, k=k, lda=m if ak else (lda_pad or k), ldb=n if bk else k, ldc=n, a_kouter=bool(ak),
+    f = lambda: ops.gemm(A, B, C, m=m, n=n, k=k, lda=m if ak else (0 if lda_pad < 0 else (lda_pad or k)), ldb=n if bk else k, ldc=n, a_kouter=bool(ak),
                          b_kouter=bool(bk), dtype=dt, out_dtype=odt, bias=bias)
     f()
     torch.cuda.synchronize()
@@ -54,7 +56,7 @@ if __name__ == "__main__":
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--regstage", default="", help="TT_GEMM_REGSTAGE value (9 = no epilogue, timing only)")
-    ap.add_argument("--lda-pad", type=int, default=0, help="A row stride in elements (K-contig A)")
+    ap.add_argument("--lda-pad", type=int, default=0, help="A row stride in elements (K-contig A); -1: lda 0, one row")
     a = ap.parse_args()
     if a.regstage:
         os.environ["TT_GEMM_REGSTAGE"] = a.regstage

@@ -39,6 +39,47 @@ def test_gemm_layouts(dt, akout, bkout, m, n, k):
     assert rel_err(C, ref) < (1e-5 if dt == torch.float32 else 2e-2)
 
 
+@pytest.mark.parametrize("a3", [0, 1])
+@pytest.mark.parametrize("akout,bkout,dt", [(0, 0, torch.bfloat16), (0, 1, torch.bfloat16), (1, 0, torch.bfloat16),
+                                            (1, 1, torch.bfloat16), (0, 0, torch.float32)])
+def test_gemm_big_tiles(akout, bkout, dt, a3):
+    """>= 256 tiles of 256x256 with a long K run the 8-phase loop of gemm_kernel (not the
+    persistent short-K kernel): ragged M/N/K tails, bias, alpha; a3 1: A prefetched two
+    K-tiles ahead through a 3-slot ring (option gemm_a3), 0: the 2-slot schedule."""
+    from two_towers_amd._lib import option
+    m, n, k = 4200, 4136, 2056
+    g = torch.Generator().manual_seed(21)
+    A = torch.randn(m, k, generator=g).to(dt).float()
+    B = torch.randn(n, k, generator=g).to(dt).float()
+    bias = torch.randn(n, generator=g)
+    Ad = (A.t().contiguous() if akout else A).to(DEV, dt)
+    Bd = (B.t().contiguous() if bkout else B).to(DEV, dt)
+    C = torch.empty(m, n, device=DEV)
+    with option("gemm_a3", a3):
+        ops.gemm([Ad], [Bd], [C], m=m, n=n, k=k, lda=m if akout else k, ldb=n if bkout else k, ldc=n,
+                 a_kouter=bool(akout), b_kouter=bool(bkout), dtype=dt, out_dtype=torch.float32, bias=[bias.to(DEV)],
+                 alpha=0.5, splits=1)
+    ref = 0.5 * (A @ B.t()) + bias
+    assert rel_err(C, ref) < 1e-5, rel_err(C, ref)
+
+
+@pytest.mark.parametrize("a3", [0, 1])
+def test_gemm_big_tiles_splitk_tn(a3):
+    """The weight-gradient shape class: TN (both operands K-outer), split-K over >= 256
+    workgroups of 256x256 tiles, fp32 partials summed by splitk_reduce_kernel."""
+    from two_towers_amd._lib import option
+    m, n, k = 1536, 1032, 16384
+    g = torch.Generator().manual_seed(22)
+    A = torch.randn(k, m, generator=g).to(torch.bfloat16).float()
+    B = torch.randn(k, n, generator=g).to(torch.bfloat16).float()
+    C = torch.empty(m, n, device=DEV)
+    with option("gemm_a3", a3):
+        ops.gemm([A.to(DEV, torch.bfloat16)], [B.to(DEV, torch.bfloat16)], [C], m=m, n=n, k=k, lda=m, ldb=n, ldc=n,
+                 a_kouter=True, b_kouter=True, dtype=torch.bfloat16, out_dtype=torch.float32)  # splits picked: 17
+    ref = A.t() @ B
+    assert rel_err(C, ref) < 1e-5, rel_err(C, ref)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_gemm_splitk_bias_accum(dt):
     g = torch.Generator().manual_seed(1)

@@ -20,6 +20,7 @@ enum Opt {
   OPT_GRU_BWD_BIG,      // 0: 128x128 backward step kernels instead of 256x256
   OPT_GRU_BWD_STREAMS,  // 1: one stream chain for the 128x128 backward
   OPT_GEMM_PERSIST,     // 0: no persistent short-K GEMM
+  OPT_GEMM_A3,          // 1: 256x256 GEMM with A prefetched two K-tiles ahead (3-slot A ring)
   OPT_GEMM_REGSTAGE,    // 1/2: force register staging / 128-tiles (9: no epilogue, timing)
   OPT_GEMM_STREAM_OUT,  // 0: no write-through output stores
   OPT_HN_GEMM,          // 1: hard-negative top-k through GEMM + split top-k, no scan

@@ -30,7 +30,7 @@ constexpr OptDef kOpts[OPT_N] = {
     {"gru_step", "TT_GRU_STEP", 0},         {"gru_depth", "TT_GRU_DEPTH", 4},
     {"gru_stagger", "TT_GRU_STAGGER", 0},   {"gru_bwd_rows", "TT_GRU_BWD_ROWS", 128},
     {"gru_bwd_big", "TT_GRU_BWD_BIG", 1},   {"gru_bwd_streams", "TT_GRU_BWD_STREAMS", 2},
-    {"gemm_persist", "TT_GEMM_PERSIST", 1}, {"gemm_regstage", "TT_GEMM_REGSTAGE", 0},
+    {"gemm_persist", "TT_GEMM_PERSIST", 1}, {"gemm_a3", "TT_GEMM_A3", 1}, {"gemm_regstage", "TT_GEMM_REGSTAGE", 0},
     {"gemm_stream_out", "TT_GEMM_STREAM_OUT", 1}, {"hn_gemm", "TT_HN_GEMM", 0},
     {"gru_bwd_persist", "TT_GRU_BWD_PERSIST", 1}, {"gru_bwd_r64", "TT_GRU_BWD_R64", 0},
     {"gru_bwd_phase", "TT_GRU_BWD_PHASE", 0},     {"gru_fwd_step_rows", "TT_GRU_FWD_STEP_ROWS", 0},
@@ -107,11 +107,12 @@ using ttg::xcd_remap;
 #define TT_GEMM_BAL true
 #endif
 
-template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO, int TBM, int TBN, int WGM, int WGN, bool DMA>
+template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO, int TBM, int TBN, int WGM, int WGN, bool DMA,
+          bool A3 = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_kernel(GemmArgs g) {
   using ML = std::conditional_t<
       DMA,
-      std::conditional_t<TBM == 256 && TBN == 256 && WGM == 2 && WGN == 4, ttg::Loop8<T, AKO, BKO, TT_GEMM_BAL>,
+      std::conditional_t<TBM == 256 && TBN == 256 && WGM == 2 && WGN == 4, ttg::Loop8<T, AKO, BKO, TT_GEMM_BAL, A3>,
                          ttg::DLoop<T, AKO, BKO, TBM, TBN, WGM, WGN>>,
       ttg::MainLoop<T, AKO, BKO, TBM, TBN>>;
   static_assert(DMA || (TBM == 128 && TBN == 128 && WGM == 2 && WGN == 2), "register path is 128x128");
@@ -262,13 +263,17 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_kernel(GemmArgs g) {
 // i prefetch the first K-tiles of tile i+nwg (their pieces re-resolved on the fly), so
 // tile i's epilogue (32-row LDS passes, separate 32 KiB) runs while tile i+nwg's first
 // half-tiles land. No split-K, no accumulate-into-C (those use gemm_kernel).
-template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO>
+// A3: A prefetched two K-tiles ahead through a 3-slot ring (Loop8 A3 layout, 160 KiB);
+// the epilogue then stages in the A slot the tile's last K-tile has just consumed, which
+// the next tile's first K-tile refills only after the epilogue's last barrier.
+template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO, bool A3>
 __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
-  using L8 = ttg::Loop8<T, AKO, BKO>;
+  using L8 = ttg::Loop8<T, AKO, BKO, false, A3>;
   using Piece = typename L8::Piece;
-  constexpr int STG = 32 * 256 * 4;
+  constexpr int STG = A3 ? 0 : 32 * 256 * 4;
+  static_assert(!A3 || 2 * L8::HALF >= 32 * 256 * 4, "staging fits an A slot");
   __shared__ __attribute__((aligned(16))) char lds[L8::LDS_BYTES + STG];
-  float* stg = reinterpret_cast<float*>(lds + L8::LDS_BYTES);
+  float* stg = reinterpret_cast<float*>(lds + L8::LDS_BYTES);  // !A3; A3: set per tile
   const int nwg = gridDim.x;
   const int w = xcd_remap(blockIdx.x, nwg);
   if (w >= ntiles) return;
@@ -324,18 +329,31 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
   long da = ttg::KTB, db = ttg::KTB;
   if constexpr (AKO) da = (long)L8::KTE * g.lda * (long)sizeof(T);
   if constexpr (BKO) db = (long)L8::KTE * g.ldb * (long)sizeof(T);
-  L8::issue_half(la, pa0, 0, da, base);
-  L8::issue_half(la, pa1, 0, da, base + L8::HALF);
-  L8::issue_half(lb, pb0, 0, db, base + 2 * L8::HALF);
-  L8::issue_half(lb, pb1, 0, db, base + 3 * L8::HALF);
-  L8::issue_half(lb, pb0, 1, db, base + L8::SLOT + 2 * L8::HALF);
-  L8::issue_half(lb, pb1, 1, db, base + L8::SLOT + 3 * L8::HALF);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  if constexpr (A3) {
+    L8::issue_half(la, pa0, 0, da, base);
+    L8::issue_half(la, pa1, 0, da, base + L8::HALF);
+    L8::issue_half(lb, pb0, 0, db, base + L8::BOFF);
+    L8::issue_half(lb, pb1, 0, db, base + L8::BOFF + L8::HALF);
+    L8::issue_half(la, pa0, 1, da, base + 2 * L8::HALF);
+    L8::issue_half(la, pa1, 1, da, base + 3 * L8::HALF);
+    L8::issue_half(lb, pb0, 1, db, base + L8::BOFF + 2 * L8::HALF);
+    L8::issue_half(lb, pb1, 1, db, base + L8::BOFF + 3 * L8::HALF);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    L8::issue_half(la, pa0, 0, da, base);
+    L8::issue_half(la, pa1, 0, da, base + L8::HALF);
+    L8::issue_half(lb, pb0, 0, db, base + 2 * L8::HALF);
+    L8::issue_half(lb, pb1, 0, db, base + 3 * L8::HALF);
+    L8::issue_half(lb, pb0, 1, db, base + L8::SLOT + 2 * L8::HALF);
+    L8::issue_half(lb, pb1, 1, db, base + L8::SLOT + 3 * L8::HALF);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  }
   __builtin_amdgcn_s_barrier();
   const bool late = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;  // wave row 1
   if (late) __builtin_amdgcn_s_barrier();
 
   int git = 0;  // running K-tile index of the stream (slot parity)
+  int as = 0;   // A3: A slot of the stream's current K-tile (git mod 3)
   int ra_off = 0, rb_off = 0;  // K-tile index of the A / B pieces' tile start in this tile's terms
   for (int q = w; q < ntiles; q += nwg) {
     const int qn = q + nwg;
@@ -346,7 +364,52 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     uint4 fa[2][4], fb[2][4];
-    for (int r = 0; r < nk; ++r, ++git) {
+    if constexpr (A3) {
+      for (int r = 0; r < nk; ++r, ++git) {
+        const int an = as == 0 ? 2 : as - 1;  // slot of K-tile r+2 = slot of r-1
+        const int bs = git & 1;
+        const char* ia = lds + as * (2 * L8::HALF) + wr * L8::HALF;
+        const char* ib = lds + L8::BOFF + bs * (2 * L8::HALF) + bh * L8::HALF;
+        const uint32_t anx = base + (uint32_t)an * (2 * L8::HALF);
+        const uint32_t bcur = base + L8::BOFF + (uint32_t)bs * (2 * L8::HALF);
+        // the stream's A and B K-tile r+2 belong to tile qn once r + 2 == nk
+        if (r + 2 == nk) {
+          la = loader_a(qn);
+          L8::template init_half<AKO>(la, 0, nk, g.K, 0, pa0);
+          L8::template init_half<AKO>(la, 0, nk, g.K, 128, pa1);
+          ra_off = nk;
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) fa[ks][i] = ttg::frag2<T, AKO>(ia, 16 * i, ks);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) fb[ks][j] = ttg::frag2<T, BKO>(ib, bc + 16 * j, ks);
+        }
+        L8::issue_half(la, pa0, r + 2 - ra_off, da, anx);
+        L8::quad(0, 0, fa, fb, acc);
+        L8::issue_half(la, pa1, r + 2 - ra_off, da, anx + L8::HALF);
+        L8::quad(0, 1, fa, fb, acc);
+        if (r + 2 == nk) {
+          lb = loader_b(qn);
+          L8::template init_half<BKO>(lb, 0, nk, g.K, 0, pb0);
+          L8::template init_half<BKO>(lb, 0, nk, g.K, 128, pb1);
+          rb_off = nk;
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) fa[ks][i] = ttg::frag2<T, AKO>(ia, 64 + 16 * i, ks);
+        L8::issue_half(lb, pb0, r + 2 - rb_off, db, bcur);
+        L8::quad(1, 1, fa, fb, acc);
+        L8::issue_half(lb, pb1, r + 2 - rb_off, db, bcur + L8::HALF);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        L8::quad(1, 0, fa, fb, acc);
+        if (r + 1 == nk) stg = reinterpret_cast<float*>(lds + as * (2 * L8::HALF));  // consumed: staging
+        as = as == 2 ? 0 : as + 1;
+      }
+    }
+    for (int r = 0; r < (A3 ? 0 : nk); ++r, ++git) {
       const int cs = git & 1;
       const uint32_t cur = base + cs * L8::SLOT, nxt = base + (cs ^ 1) * L8::SLOT;
       const char* ia = lds + cs * L8::SLOT + wr * L8::HALF;
@@ -477,11 +540,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* ws, lon
   }
 }
 
-template <typename T, typename TO, int TBM, int TBN, int WGM, int WGN, bool DMA>
+template <typename T, typename TO, int TBM, int TBN, int WGM, int WGN, bool DMA, bool A3 = false>
 int launch_t(int akout, int bkout, bool shift, const GemmArgs& g, long nwg, hipStream_t st) {
   dim3 grid((unsigned)nwg), blk(64 * WGM * WGN);
 #define TT_L(AK, BK, SH) \
-  hipLaunchKernelGGL((gemm_kernel<T, AK, BK, SH, TO, TBM, TBN, WGM, WGN, DMA>), grid, blk, 0, st, g)
+  hipLaunchKernelGGL((gemm_kernel<T, AK, BK, SH, TO, TBM, TBN, WGM, WGN, DMA, A3>), grid, blk, 0, st, g)
   if (!akout && !bkout) TT_L(false, false, false);
   else if (!akout && bkout && !shift) TT_L(false, true, false);
   else if (!akout && bkout && shift) TT_L(false, true, true);
@@ -500,13 +563,20 @@ inline bool use_big(int m, int n, long tiles256) { return m >= 256 && n >= 256 &
 template <typename T, typename TO>
 int launch_persist(int akout, int bkout, bool shift, const GemmArgs& g, int ntiles, hipStream_t st) {
   dim3 grid((unsigned)std::min(ntiles, 256)), blk(512);
-#define TT_L(AK, BK, SH) hipLaunchKernelGGL((gemm_persist<T, AK, BK, SH, TO>), grid, blk, 0, st, g, ntiles)
-  if (!akout && !bkout) TT_L(false, false, false);
-  else if (!akout && bkout && !shift) TT_L(false, true, false);
-  else if (!akout && bkout && shift) TT_L(false, true, true);
-  else if (akout && !bkout) TT_L(true, false, false);
-  else if (akout && bkout && !shift) TT_L(true, true, false);
-  else TT_L(true, true, true);
+#define TT_L(AK, BK, SH, A3) hipLaunchKernelGGL((gemm_persist<T, AK, BK, SH, TO, A3>), grid, blk, 0, st, g, ntiles)
+#define TT_L2(AK, BK, SH) \
+  do {                     \
+    if (a3) TT_L(AK, BK, SH, true); \
+    else TT_L(AK, BK, SH, false);   \
+  } while (0)
+  const bool a3 = tt::opt(tt::OPT_GEMM_A3) != 0;
+  if (!akout && !bkout) TT_L2(false, false, false);
+  else if (!akout && bkout && !shift) TT_L2(false, true, false);
+  else if (!akout && bkout && shift) TT_L2(false, true, true);
+  else if (akout && !bkout) TT_L2(true, false, false);
+  else if (akout && bkout && !shift) TT_L2(true, true, false);
+  else TT_L2(true, true, true);
+#undef TT_L2
 #undef TT_L
   TT_CHECK_LAUNCH("gemm_persist");
   return 0;
@@ -526,8 +596,10 @@ int launch_gemm(int akout, int bkout, bool shift, GemmArgs& g, int nbatch, hipSt
   if (dma && persist_ok && g.force_regstage == 0 && g.splits == 1 && !g.beta && nk >= 2 && nk <= 24 && t256 >= 512 &&
       use_big(g.M, g.N, t256))
     return launch_persist<T, TO>(akout, bkout, shift, g, (int)t256, st);
-  if (dma && g.force_regstage != 2 && use_big(g.M, g.N, t256))
+  if (dma && g.force_regstage != 2 && use_big(g.M, g.N, t256)) {
+    if (tt::opt(tt::OPT_GEMM_A3)) return launch_t<T, TO, 256, 256, 2, 4, true, true>(akout, bkout, shift, g, t256, st);
     return launch_t<T, TO, 256, 256, 2, 4, true>(akout, bkout, shift, g, t256, st);
+  }
   const long t128 = (long)tt_ceil_div(g.M, 128) * tt_ceil_div(g.N, 128) * nbatch * g.splits;
   if (dma) return launch_t<T, TO, 128, 128, 2, 2, true>(akout, bkout, shift, g, t128, st);
   return launch_t<T, TO, 128, 128, 2, 2, false>(akout, bkout, shift, g, t128, st);

@@ -448,9 +448,14 @@ struct DLoop {
 // 256^2 8-phase template: counted vmcnt, raw s_barrier, all LDS in one array). Every wave
 // issues 2 DMAs per half-tile, always (a K-tile past the slice end reads the zero page),
 // so the counts are exact.
-template <typename T, bool AKO, bool BKO, bool BAL = false>
+// A3: A gets a 3-slot ring (prefetched two K-tiles ahead, like B) in 160 KiB: A slots at
+// 0, 32, 64 KiB, B slots at 96, 128 KiB. A of K-tile r+2 goes into the slot K-tile r-1
+// used (both wave rows finished reading it one interval before this K-tile's P1); every
+// K-tile then has 8 DMAs per wave in flight at its wait (vmcnt(8)).
+template <typename T, bool AKO, bool BKO, bool BAL = false, bool A3 = false>
 struct Loop8 {
-  static constexpr int HALF = 16384, SLOT = 4 * HALF, LDS_BYTES = 2 * SLOT;
+  static constexpr int HALF = 16384, SLOT = 4 * HALF, LDS_BYTES = A3 ? 10 * HALF : 2 * SLOT;
+  static constexpr int BOFF = 6 * HALF;  // A3: first B slot
   static constexpr int TM = 8, TN = 4;
   static constexpr int KTE = KTB / (int)sizeof(T);  // K elements per K-tile
 
@@ -551,6 +556,10 @@ struct Loop8 {
     long da = KTB, db = KTB;  // K-contig operands advance 128 B per K-tile
     if constexpr (AKO) da = (long)KTE * la.ld * (long)sizeof(T);
     if constexpr (BKO) db = (long)KTE * lb.ld * (long)sizeof(T);
+    if constexpr (A3) {
+      run3(la, lb, kt1 - kt0, lds, base, da, db, pa0, pa1, pb0, pb1, acc);
+      return;
+    }
     issue_half(la, pa0, 0, da, base);
     issue_half(la, pa1, 0, da, base + HALF);
     issue_half(lb, pb0, 0, db, base + 2 * HALF);
@@ -621,6 +630,67 @@ struct Loop8 {
       issue_half(lb, pb1, r + 2, db, cur + 3 * HALF);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       quad(1, 0, fa, fb, acc);
+    }
+    if (!late) __builtin_amdgcn_s_barrier();  // re-align the two wave rows
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing zero-page DMAs before LDS reuse
+    __builtin_amdgcn_s_barrier();
+  }
+
+  // The A3 schedule (balanced reads as BAL): per K-tile r, P1 reads A rows 0-63 + B
+  // columns 0-31 and restages A0 of r+2, P2 reads B columns 32-63 and restages A1 of r+2,
+  // P3 reads A rows 64-127, P4 restages both B halves of r+2 into B's current slot and
+  // waits for K-tile r+1 with the 8 youngest DMAs (A and B of r+2) still in flight.
+  template <class LA, class LB>
+  TT_DEV static void run3(const LA& la, const LB& lb, int nk, char* lds, uint32_t base, long da, long db,
+                          const Piece (&pa0)[2], const Piece (&pa1)[2], const Piece (&pb0)[2], const Piece (&pb1)[2],
+                          f32x4 (&acc)[TM][TN]) {
+    const int wave = threadIdx.x >> 6;
+    const int wr = wave >> 2, bh = (wave & 3) >> 1, bc = (wave & 1) * 64;
+    issue_half(la, pa0, 0, da, base);
+    issue_half(la, pa1, 0, da, base + HALF);
+    issue_half(lb, pb0, 0, db, base + BOFF);
+    issue_half(lb, pb1, 0, db, base + BOFF + HALF);
+    issue_half(la, pa0, 1, da, base + 2 * HALF);
+    issue_half(la, pa1, 1, da, base + 3 * HALF);
+    issue_half(lb, pb0, 1, db, base + BOFF + 2 * HALF);
+    issue_half(lb, pb1, 1, db, base + BOFF + 3 * HALF);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const bool late = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;  // wave row 1
+    if (late) __builtin_amdgcn_s_barrier();
+    uint4 fa[2][4], fb[2][4];
+    int as = 0;  // A slot of K-tile r (r mod 3)
+    for (int r = 0; r < nk; ++r) {
+      const int an = as == 0 ? 2 : as - 1;  // slot of K-tile r+2 = slot of r-1
+      const int bs = r & 1;
+      const char* ia = lds + as * (2 * HALF) + wr * HALF;
+      const char* ib = lds + BOFF + bs * (2 * HALF) + bh * HALF;
+      const uint32_t anx = base + (uint32_t)an * (2 * HALF), bcur = base + BOFF + (uint32_t)bs * (2 * HALF);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[ks][i] = frag2<T, AKO>(ia, 16 * i, ks);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb[ks][j] = frag2<T, BKO>(ib, bc + 16 * j, ks);
+      }
+      issue_half(la, pa0, r + 2, da, anx);
+      quad(0, 0, fa, fb, acc);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 2; j < 4; ++j) fb[ks][j] = frag2<T, BKO>(ib, bc + 16 * j, ks);
+      issue_half(la, pa1, r + 2, da, anx + HALF);
+      quad(0, 1, fa, fb, acc);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[ks][i] = frag2<T, AKO>(ia, 64 + 16 * i, ks);
+      quad(1, 1, fa, fb, acc);
+      issue_half(lb, pb0, r + 2, db, bcur);
+      issue_half(lb, pb1, r + 2, db, bcur + HALF);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      quad(1, 0, fa, fb, acc);
+      as = as == 2 ? 0 : as + 1;
     }
     if (!late) __builtin_amdgcn_s_barrier();  // re-align the two wave rows
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing zero-page DMAs before LDS reuse

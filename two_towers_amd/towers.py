@@ -152,8 +152,9 @@ def _gru_layer_fwd(cfg, xs, K, ldx, packs, layer, B, T, seeds, want_x1):
     BT = B * T
     G = [_alloc((BT, 6 * H), dt, dev) for _ in range(n)]
     esz = 2 if dt == torch.bfloat16 else 4
-    with timing.region(f"input_proj_l{layer}", 1, 2.0 * BT * 6 * H * K * n,
-                       float(n * esz * (BT * K + 6 * H * K + BT * 6 * H))):
+    kr = cfg.E if layer == 0 else K  # algorithmic work counts the real columns, not the padding
+    with timing.region(f"input_proj_l{layer}", 1, 2.0 * BT * 6 * H * kr * n,
+                       float(n * esz * (BT * kr + 6 * H * kr + BT * 6 * H))):
         ops.gemm(xs, [p.wih[layer] for p in packs], G, m=BT, n=6 * H, k=K, lda=ldx, ldb=K, ldc=6 * H,
                  a_kouter=False, b_kouter=False, dtype=dt, out_dtype=dt, bias=[p.bias[layer] for p in packs])
     Y = [_alloc((BT, 2 * H), dt, dev) for _ in range(n)]
@@ -229,7 +230,7 @@ def _gru_layer_bwd(cfg, layer, B, T, S, Y, dY, dfinal, packs):
     return dG, dbih, dbhh
 
 
-def _weight_grads(cfg, B, T, dG, Xin, K, ldx, Y):
+def _weight_grads(cfg, B, T, dG, Xin, K, ldx, Y, kr=None):
     """dW_ih = dG^T Xin, dW_hh = dGH^T Y_{t-1} for all (tower, dir) in two batched TN GEMMs."""
     n, H, dt, dev = cfg.ntowers, cfg.H, cfg.dtype, dG[0].device
     BT = B * T
@@ -247,8 +248,9 @@ def _weight_grads(cfg, B, T, dG, Xin, K, ldx, Y):
             c_hh.append(dWhh[ti][d])
             sh.append(-1 if d == 0 else 1)
     esz = 2 if dt == torch.bfloat16 else 4
-    with timing.region("wgrad_ih", 1, 2.0 * 3 * H * K * BT * 2 * n,
-                       float(n * (esz * BT * (6 * H + K) + 2 * 3 * H * K * 4))):
+    kr = K if kr is None else kr  # layer 0: the real embedding columns, not the padding
+    with timing.region("wgrad_ih", 1, 2.0 * 3 * H * kr * BT * 2 * n,
+                       float(n * (esz * BT * (6 * H + kr) + 2 * 3 * H * kr * 4))):
         ops.gemm(a_ih, b_ih, c_ih, m=3 * H, n=K, k=BT, lda=8 * H, ldb=ldx, ldc=K, a_kouter=True, b_kouter=True,
                  dtype=dt, out_dtype=torch.float32)
     with timing.region("wgrad_hh", 1, 2.0 * 3 * H * H * BT * 2 * n,
@@ -387,7 +389,7 @@ class TowersFn(torch.autograd.Function):
         # ---- GRU layer 0
         dG0, dbih0, dbhh0 = _gru_layer_bwd(cfg, 0, B, T, S0, Y0, dY0, None, packs)
         del dY0
-        dWih0, dWhh0 = _weight_grads(cfg, B, T, dG0, X0, Ep, Ep, Y0)
+        dWih0, dWhh0 = _weight_grads(cfg, B, T, dG0, X0, Ep, Ep, Y0, kr=E)
         gl0 = [{} for _ in range(n)]
         _layer_grads(gl0, 0, E, Ep, dWih0, dWhh0, dbih0, dbhh0)
         if red is not None:

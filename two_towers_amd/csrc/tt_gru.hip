@@ -1102,10 +1102,12 @@ TT_DEV void fwd_kstep(const bf16_t* W, int H, int Q, int q, int kt, bool mm, con
       for (int i = 0; i < 2; ++i) fa[i] = ttg::frag<bf16_t, false>(ia, wm + 16 * i, ks);
 #pragma unroll
       for (int j = 0; j < 3; ++j) fb[j] = ttg::frag<bf16_t, false>(ib, wn + 16 * j, ks);
+      __builtin_amdgcn_s_setprio(1);  // ≈ 1 % (profiles/r02_gru_fwd_prio_ab.txt)
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j) acc[i][j] = ttg::mma<bf16_t>(fa[i], fb[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
     }
   }
   TT_STAMP(t1);

@@ -11,13 +11,13 @@ from two_towers_amd import ops  # noqa: E402
 
 SHAPES = {  # name: (m, n, k, a_kouter, b_kouter, nbatch, out_bf16)
     "input_proj_l1": (524288, 3072, 1024, 0, 0, 2, 1),
-    "input_proj_l0": (524288, 3072, 304, 0, 0, 2, 1),
+    "input_proj_l0": (524288, 3072, 320, 0, 0, 2, 1),  # Ep 320 since round 2 (304 before)
     "dgrad_l1": (524288, 1024, 3072, 0, 1, 1, 1),
     "wgrad_ih1": (1536, 1024, 524288, 1, 1, 4, 0),
     "wgrad_hh": (1536, 512, 524288, 1, 1, 4, 0),
     "square8k": (8192, 8192, 8192, 0, 0, 1, 1),
-    # diagnostics: K padded to whole 128-B lines; the l1 FLOPs with a B small enough for L2
-    "input_proj_l0_k320": (524288, 3072, 320, 0, 0, 2, 1),
+    # diagnostics: the round-1 16-byte padding; the l1 FLOPs with a B small enough for L2
+    "input_proj_l0_k304": (524288, 3072, 304, 0, 0, 2, 1),
     "proj_l1_n768": (2097152, 768, 1024, 0, 0, 2, 1),
     "sq_k1024": (16384, 16384, 1024, 0, 0, 1, 1),
 }

@@ -5,7 +5,7 @@ import torch
 
 SHAPES = {  # name: (m, n, k, a_kouter, b_kouter, nbatch)
     "input_proj_l1": (524288, 3072, 1024, 0, 0, 2),
-    "input_proj_l0": (524288, 3072, 304, 0, 0, 2),
+    "input_proj_l0": (524288, 3072, 320, 0, 0, 2),
     "dgrad_l1": (524288, 1024, 3072, 0, 1, 1),
     "wgrad_ih1": (1536, 1024, 524288, 1, 1, 4),
     "wgrad_hh": (1536, 512, 524288, 1, 1, 4),

@@ -123,6 +123,19 @@ def test_oracle_is_not_imported_by_the_product():
                     assert not any(m.startswith("oracle") for m in mods), f
 
 
+def test_embedding_rows_are_padded_to_whole_lines():
+    """Gathered embedding rows (and W_ih l0's K) are padded to 128-byte lines, so every
+    layer-0 GEMM K-tile starts on a cache line and the padding adds no K-tile."""
+    from two_towers_amd import ops
+    assert ops.pad_cols(300, torch.bfloat16) == 320 and ops.pad_cols(300, torch.float32) == 320
+    assert ops.pad_cols(64, torch.bfloat16) == 64 and ops.pad_cols(65, torch.bfloat16) == 128
+    for e in (1, 48, 300, 301, 512):
+        for dt in (torch.bfloat16, torch.float32):
+            ep = ops.pad_cols(e, dt)
+            esz = 2 if dt == torch.bfloat16 else 4
+            assert ep >= e and (ep * esz) % 128 == 0 and (ep - e) * esz < 128
+
+
 def test_split_k_picker_fills_the_chip():
     """Host-side launch heuristics: a small-M/N, long-K weight gradient (the projection
     head's dW, 8 or 32 tiles) must be split over K; big problems are not split."""

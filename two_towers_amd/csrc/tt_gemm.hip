@@ -582,6 +582,9 @@ int launch_persist(int akout, int bkout, bool shift, const GemmArgs& g, int ntil
   return 0;
 }
 
+#ifndef TT_PERSIST_MAXK
+#define TT_PERSIST_MAXK 24
+#endif
 template <typename T, typename TO>
 int launch_gemm(int akout, int bkout, bool shift, GemmArgs& g, int nbatch, hipStream_t st) {
   constexpr int EPC = 16 / (int)sizeof(T);
@@ -593,7 +596,7 @@ int launch_gemm(int akout, int bkout, bool shift, GemmArgs& g, int nbatch, hipSt
   // slower at 48 and 128), no split-K, no accumulate (env TT_GEMM_PERSIST=0 disables)
   const bool persist_ok = tt::opt(tt::OPT_GEMM_PERSIST) != 0;
   const int nk = (g.K * (int)sizeof(T) + ttg::KTB - 1) / ttg::KTB;
-  if (dma && persist_ok && g.force_regstage == 0 && g.splits == 1 && !g.beta && nk >= 2 && nk <= 24 && t256 >= 512 &&
+  if (dma && persist_ok && g.force_regstage == 0 && g.splits == 1 && !g.beta && nk >= 2 && nk <= TT_PERSIST_MAXK && t256 >= 512 &&
       use_big(g.M, g.N, t256))
     return launch_persist<T, TO>(akout, bkout, shift, g, (int)t256, st);
   if (dma && g.force_regstage != 2 && use_big(g.M, g.N, t256)) {

@@ -1106,7 +1106,8 @@ TT_DEV void fwd_kstep(const bf16_t* W, int H, int Q, int q, int kt, bool mm, con
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) acc[i][j] = ttg::mma<bf16_t>(fa[i], fb[j], acc[i][j]);
+        for (int j = 0; j < 3; ++j)  // operands swapped: acc holds C^T (4 gate columns of a row per lane)
+          acc[i][j] = ttg::mma<bf16_t>(fb[j], fa[i], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
     }
   }
@@ -1233,13 +1234,14 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
 #undef TT_KS
         TT_STAMP(e0);
         // gates -> LDS (fp32), then per-thread rows
+        // (C^T accumulators: one 16-byte store per block instead of four 4-byte ones; ≈ 0.4 %,
+        // bit-identical, profiles/r02_gru_fwd_ct_ab.txt)
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int j = 0; j < 3; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              stg[stg_off(wm + 16 * i + 4 * (lane >> 4) + r, wn + 16 * j + (lane & 15))] = acc[i][j][r];
+            *reinterpret_cast<f32x4*>(stg + stg_off(wm + 16 * i + (lane & 15), wn + 16 * j + 4 * (lane >> 4))) =
+                acc[i][j];
         __syncthreads();
         TT_STAMP(e1);
         TT_ACC(3, e1 - e0);  // gate staging + barrier

@@ -673,7 +673,8 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][jp + j] = ttg::mma<bf16_t>(fa[i], fb[j], acc[i][jp + j]);
+            for (int j = 0; j < 2; ++j)  // C^T accumulators: 4 consecutive units of one row per lane
+              acc[i][jp + j] = ttg::mma<bf16_t>(fb[j], fa[i], acc[i][jp + j]);
           __builtin_amdgcn_s_setprio(0);
         }
       }
@@ -689,14 +690,16 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
     const __amdgpu_buffer_rsrc_t ry = tt_rsrc_n(s > 0 ? Y + ((long)m0 * T_ + tp) * a.ldy : S, s > 0);
     const __amdgpu_buffer_rsrc_t grs = tt_rsrc(DGXw + trow * a.ldd);
     uint32_t* L16 = reinterpret_cast<uint32_t*>(lds);
+    // the accumulator as a bf16 image: one 8-byte store of 4 units per (row block, column block)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int jc = 0; jc < C::NCB; ++jc)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          reinterpret_cast<bf16_t*>(lds)[(wr * 64 + 16 * i + 4 * (lane >> 4) + e) * C::LDB + wc * (H / 4) + 16 * jc +
-                                         (lane & 15)] = f2bf(acc[i][jc][e]);
+      for (int jc = 0; jc < C::NCB; ++jc) {
+        const uint32_t w0 = (uint32_t)f2bf(acc[i][jc][0]) | ((uint32_t)f2bf(acc[i][jc][1]) << 16);
+        const uint32_t w1 = (uint32_t)f2bf(acc[i][jc][2]) | ((uint32_t)f2bf(acc[i][jc][3]) << 16);
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(lds) + (wr * 64 + 16 * i + (lane & 15)) * C::LDB +
+                                  wc * (H / 4) + 16 * jc + 4 * (lane >> 4)) = make_uint2(w0, w1);
+      }
     __syncthreads();
     float bsum[4][8];
 #pragma unroll

@@ -198,6 +198,33 @@ def test_persistent_gru_matches_step_kernel(h, B, T):
         assert rel(g1[k], g0[k]) < 1e-4, k
 
 
+@pytest.mark.parametrize("rr", [1, 2, 3])
+def test_experimental_row_resident_forward_is_bit_identical(rr):
+    """Option gru_fwd_rr (the 128-row forward with the gates in registers, measured slower
+    and off by default): same MFMA order along K and the same gate expression as
+    gru_fwd_seq, so the forward outputs are bit-identical; the gradients agree to the
+    order of the head's atomic bias reductions (rel < 1e-5). B = 130 gives a tail tile of
+    2 rows; dropout on."""
+    E, h, B, T = 48, 256, 130, 5
+    g = torch.Generator().manual_seed(13)
+    q = torch.randn(B, T, E, generator=g).to(DEV)
+    d = torch.randn(B, T, E, generator=g).to(DEV)
+    outs = []
+    for v in (0, rr):
+        m, _ = make_model(E, h, 3)
+        m = m.to(DEV).train().set_compute_dtype(torch.bfloat16)
+        with option("gru_fwd_rr", v):
+            torch.manual_seed(5)
+            qv, dv = m(q, d)
+            loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
+            loss.backward()
+        outs.append((qv.detach().clone(), dv.detach().clone(), {k: p.grad.clone() for k, p in m.named_parameters()}))
+    (q0, d0, g0), (q1, d1, g1) = outs
+    assert torch.equal(q1, q0) and torch.equal(d1, d0)
+    for k in g0:
+        assert rel(g1[k], g0[k]) < 1e-5, k
+
+
 @pytest.mark.parametrize("B,T", [(130, 5), (520, 3)])
 def test_big_tile_gru_backward_matches_step_kernel(B, T):
     """bf16 H=512 backward on 256x256 tiles (8-phase GEMM, two-pass epilogue) vs the

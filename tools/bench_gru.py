@@ -75,6 +75,7 @@ def main():
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--variants", default="seq:0")
     ap.add_argument("--bwd-variants", default="128:0:2")
+    ap.add_argument("--check", default="", help="kind:kind - compare Y / X1 / S of two forward kinds")
     a = ap.parse_args()
     dev = torch.device("cuda")
     recs, keep = setup(a.B, a.T, a.H, dev)
@@ -106,11 +107,27 @@ def main():
         ms = s.elapsed_time(e) / a.iters
         print(json.dumps({"bwd_rows": v, "ms": round(ms, 3)}), flush=True)
         del brecs, bkeep
+    if a.check:
+        outs = []
+        for kind in a.check.split(":"):
+            set_option("gru_step", 1 if kind == "step" else 0)
+            set_option("gru_fwd_rr", {"rr": 1, "rr2": 2, "rr3": 3}.get(kind, 0))
+            set_option("gru_depth", 4)
+            for t in keep[3] + keep[4] + [x for p in keep[5] for x in p]:
+                t.fill_(float("nan"))
+            call("tt_gru_fwd", 1, recs, 4, a.B, a.T, a.H, 6 * a.H, 2 * a.H, 0.1, st)
+            torch.cuda.synchronize()
+            outs.append([t.float().clone() for t in keep[3] + keep[4] + [x for p in keep[5] for x in p]])
+        for name, x, y in zip(["Y0", "Y1", "X1_0", "X1_1", "S00", "S01", "S10", "S11"], *outs):
+            d = (x - y).abs()
+            print(json.dumps({"check": a.check, "out": name, "nan": int(torch.isnan(y).sum()), "max_abs": float(d.max()),
+                              "n_diff": int((d > 0).sum()), "ref_max": float(x.abs().max())}), flush=True)
     for v in a.variants.split(","):
         if not v:
             continue
         kind, dbg, *depth = v.split(":")
         set_option("gru_step", 1 if kind == "step" else 0)
+        set_option("gru_fwd_rr", {"rr": 1, "rr2": 2, "rr3": 3}.get(kind, 0))
         os.environ["TT_GRU_DBG"] = dbg  # read only by a -DTT_DIAG build
         set_option("gru_depth", int(depth[0]) if depth else 4)
         f = lambda: call("tt_gru_fwd", 1, recs, 4, a.B, a.T, a.H, 6 * a.H, 2 * a.H, 0.1, st)

@@ -1338,6 +1338,301 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
 #endif
 }
 
+// ---- row-resident forward with the gates in registers (R x H = 65536) -------------
+// EXPERIMENT, off by default (option gru_fwd_rr 1 / 2 / 3); bit-identical to gru_fwd_seq
+// and measured slower (profiles/r02_gru_fwd_rr_ab.txt).
+// R = 128 rows per workgroup at H = 512: twice the rows per streamed W_hh byte of
+// gru_fwd_seq. The bf16 h image (R x H x 2 = 128 KiB) and a 2-stage ring of 32-deep
+// W_hh K-tiles (2 x 12 KiB) fill the LDS, so there is no room for fp32 gate staging: the
+// B-image rows are ordered [slab of 16 units][gate][16 units] and the accumulators hold
+// C^T, so a lane owns r, z and n of 4 consecutive units of MI rows per slab and updates
+// them in registers with 8-byte G / Y / S accesses. Waves as WM (rows) x WN (slab
+// groups); NT 256 = one wave per SIMD, NT 512 = two per SIMD. The fp32 state alone is 128
+// registers per lane at NT 512, so the epilogue spills (46-136 registers by variant).
+// Measured at configs[2] (4 recurrences, B 8192, T 64): 15.1-17.6 ms vs 7.25 for
+// gru_fwd_seq; with the Y / S / X1 stores compiled out (-DRR_DBG=1) the 2 x 4 layout
+// takes 6.50 ms, so the 8-byte stores (16 rows x 32 B per wave instruction, each 128-byte
+// line completed by four waves) cost ~9.6 ms, not the W_hh stream. H 1024 at 64 rows
+// measured W_hh-bound: 92 vs 48 ms per layer at configs[4] (6 MiB W_hh per recurrence
+// does not stay in a 4 MiB L2), not instantiated.
+#ifndef RR_DBG
+#define RR_DBG 0
+#endif
+constexpr int RR_KTB = 64;                // bytes per W_hh row of a 32-deep K-tile
+constexpr int RR_BST = 192 * RR_KTB;      // 12288 per stage
+// W image rows of 64 B, chunk c at c ^ ((row >> 1) & 3): conflict-free for the 16-row
+// ds_read_b128 fragment groups and the 8-lane ds_write_b128 groups
+TT_DEV int rr_w_off(int row, int c) { return row * RR_KTB + ((c ^ ((row >> 1) & 3)) << 4); }
+
+template <int H, int NT, int WN_ = NT / 128>
+struct RRCfg {
+  static constexpr int R = 65536 / H;     // batch rows per workgroup
+  static constexpr int WN = WN_;          // wave columns
+  static constexpr int WM = NT / 64 / WN; // wave rows
+  static constexpr int MI = R / WM / 16;  // 16-row fragments per wave
+  static constexpr int UG = 4 / WN;       // 16-unit slabs per wave
+  static constexpr int NB = H / 64;       // 64-unit blocks per step
+  static constexpr int NK = H / 32;       // 32-deep K-tiles per block
+  static constexpr int Q = NB * NK;       // K-tiles per step
+  static constexpr int HB = R * H * 2;    // h image bytes
+  static constexpr int LDS = HB + 2 * RR_BST;
+  static constexpr int NC = 768 / NT;     // 16-byte W chunks per thread and K-tile (1.5 -> 2)
+  static_assert(LDS <= 163840, "row-resident GRU LDS budget");
+};
+
+template <int NT>
+struct RRTile {
+  uint4 v[NT == 256 ? 3 : 2];
+};
+// per-thread byte offset of chunk id within K-tile (0, 0); the K-tile's own offset
+// (blk*64 rows, kt*32 columns) is wave-uniform and goes in soffset. NT 512: chunks t and
+// t + 512 (threads < 256; the others' second offset is out of range and reads nothing)
+template <int H>
+TT_DEV uint32_t rr_w_byte(int id) {
+  const int n = id >> 2, c = id & 3;
+  const int slab = n / 48, rem = n - slab * 48, g = rem >> 4, u = rem & 15;
+  return (uint32_t)(((g * H + slab * 16 + u) * H + c * 8) * 2);
+}
+template <int H, int NT>
+TT_DEV void rr_load_b(__amdgpu_buffer_rsrc_t rW, const uint32_t (&w)[NT == 256 ? 3 : 2], int q, RRTile<NT>& r) {
+  constexpr int NK = RRCfg<H, NT>::NK;
+  const int blk = q / NK, kt = q - blk * NK;
+  const int so = (blk * 64 * H + kt * 32) * 2;
+#pragma unroll
+  for (int c = 0; c < (NT == 256 ? 3 : 2); ++c) r.v[c] = ld16_buf(rW, w[c], so);
+}
+template <int NT>
+TT_DEV void rr_store_b(char* img, const RRTile<NT>& r) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int c = 0; c < (NT == 256 ? 3 : 1); ++c) {
+    const int id = t + NT * c;
+    *reinterpret_cast<uint4*>(img + rr_w_off(id >> 2, id & 3)) = r.v[c];
+  }
+  if (NT == 512 && t < 256) *reinterpret_cast<uint4*>(img + rr_w_off((t + 512) >> 2, t & 3)) = r.v[1];
+}
+TT_DEV uint2 ld8_buf(__amdgpu_buffer_rsrc_t r, uint32_t voff, int soff) {
+  typedef unsigned u32x2 __attribute__((vector_size(8)));
+  const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, soff, 0);
+  return make_uint2(v[0], v[1]);
+}
+TT_DEV void st8_buf(__amdgpu_buffer_rsrc_t r, uint32_t voff, int soff, uint2 v) {
+  typedef unsigned u32x2 __attribute__((vector_size(8)));
+  u32x2 w = {v.x, v.y};
+  __builtin_amdgcn_raw_buffer_store_b64(w, r, (int)voff, soff, 0);
+}
+TT_DEV uint2 pack4bf(const float (&f)[4]) {
+  return make_uint2((uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16),
+                    (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16));
+}
+TT_DEV void unpack4(uint2 v, float (&f)[4]) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xFFFF0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xFFFF0000u);
+}
+
+// One 32-deep K-tile: prefetch K-tile q+D into set Y, MFMAs on stage kt&1 (every block
+// starts on an even K-tile count), store set X (K-tile q+1) into the other stage, barrier.
+template <int H, int NT, int WN, int D>
+TT_DEV void rr_kstep(__amdgpu_buffer_rsrc_t rW, const uint32_t (&w)[NT == 256 ? 3 : 2], int q, int kt, bool mm,
+                     const char* hb, char* bst, int wm, int wn,
+                     f32x4 (&acc)[RRCfg<H, NT, WN>::MI][3 * RRCfg<H, NT, WN>::UG], RRTile<NT>& X, RRTile<NT>& Y) {
+  using C = RRCfg<H, NT, WN>;
+  const int lane = threadIdx.x & 63;
+  rr_load_b<H, NT>(rW, w, (q + D) % C::Q, Y);
+  if (mm) {  // h_{-1} = 0: the first step has no recurrent term
+    // the A tile offset is opaque to the compiler: folded into immediates it needs a
+    // second set of base registers past 64 KiB, which it hoists and spills
+    int aoff = (kt >> 1) * (C::R * ttg::KTB);
+    asm volatile("" : "+s"(aoff));
+    const char* ia = hb + aoff;
+    const char* ib = bst + (kt & 1) * RR_BST;
+    uint4 fb[3 * C::UG];
+#pragma unroll
+    for (int j = 0; j < 3 * C::UG; ++j)
+      fb[j] = *reinterpret_cast<const uint4*>(ib + rr_w_off(wn + 16 * j + (lane & 15), lane >> 4));
+#pragma unroll
+    for (int i = 0; i < C::MI; ++i) {
+      const uint4 fa = ttg::frag<bf16_t, false>(ia, wm + 16 * i, kt & 1);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < 3 * C::UG; ++j) acc[i][j] = ttg::mma<bf16_t>(fb[j], fa, acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  rr_store_b<NT>(bst + ((kt + 1) & 1) * RR_BST, X);
+  __syncthreads();
+}
+
+template <int H, int NT, int WN, int D>
+__global__ __launch_bounds__(NT) void gru_fwd_rr(FwdArgs a) {
+  using C = RRCfg<H, NT, WN>;
+  constexpr int R = C::R, MI = C::MI, NB = C::NB, NK = C::NK, UG = C::UG;
+  constexpr int NW = NT == 256 ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) char lds[C::LDS];
+  char* hb = lds;
+  char* bst = lds + C::HB;
+  const int ntm = (a.B + R - 1) / R;
+  const int id = ttg::xcd_remap(blockIdx.x, gridDim.x);
+  const int rz = id / ntm;
+  const FwdRec Rc = a.r[rz];
+  const int T_ = a.T;
+  const int m0 = (id - rz * ntm) * R;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wc = wave % WN;
+  const int wm = (wave / WN) * (R / C::WM), wn = wc * 48 * UG;
+  // first of this lane's 4 units of slab ug within a block: (wc*UG + ug)*16 + 4*(lane>>4)
+  const int ub = wc * UG * 16 + 4 * (lane >> 4);
+  const bf16_t* G = static_cast<const bf16_t*>(Rc.g);
+  bf16_t* Yw = static_cast<bf16_t*>(Rc.y);
+  bf16_t* X1 = static_cast<bf16_t*>(Rc.x1);
+  bf16_t* S = static_cast<bf16_t*>(Rc.save);
+  // buffer resources based at this workgroup's first row (see gru_fwd_seq): a tail row's
+  // offset is out of range, so its loads read zeros and its stores are dropped
+  const long r0w = (long)m0 * T_;
+  const __amdgpu_buffer_rsrc_t rW = tt_rsrc_n(Rc.whh, true);
+  const __amdgpu_buffer_rsrc_t rG = tt_rsrc_n(G + r0w * a.ldg, true);
+  const __amdgpu_buffer_rsrc_t rY = tt_rsrc_n(Yw + r0w * a.ldy, true);
+  const __amdgpu_buffer_rsrc_t rX1 = tt_rsrc_n(X1 ? X1 + r0w * a.ldy : Yw, X1 != nullptr);
+  const __amdgpu_buffer_rsrc_t rS = tt_rsrc_n(S + r0w * 4L * H, true);
+  uint32_t w[NW];
+#pragma unroll
+  for (int c = 0; c < NW; ++c) w[c] = rr_w_byte<H>(tid + NT * c);
+  if (NT == 512) w[1] = tid < 256 ? rr_w_byte<H>(tid + 512) : 0x80000000u;
+  int rl[MI];
+  bool ok[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    rl[i] = wm + 16 * i + (lane & 15);
+    ok[i] = m0 + rl[i] < a.B;
+  }
+
+  // fp32 state: hreg[i][blk][ug][e] = h(row rl[i], unit blk*64 + ub + 16*ug + e); rotated
+  // so that hreg[.][0] is always the block being updated
+  float hreg[MI][NB][UG][4];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+#pragma unroll
+      for (int u = 0; u < UG; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) hreg[i][k][u][e] = 0.f;
+
+  RRTile<NT> r0, r1, r2, r3;
+  rr_load_b<H, NT>(rW, w, 0, r0);
+  rr_store_b<NT>(bst, r0);
+  if (D >= 2) rr_load_b<H, NT>(rW, w, 1, r1);
+  if (D >= 4) {
+    rr_load_b<H, NT>(rW, w, 2, r2);
+    rr_load_b<H, NT>(rW, w, 3, r3);
+  }
+  __syncthreads();
+  // dropped stores standing in for the epilogue's, so every path into a block's first
+  // K-tiles has the same pending count (see gru_fwd_seq)
+#pragma unroll
+  for (int q = 0; q < 6 * MI * UG; ++q) st8_buf(rY, 0x80000000u + 8u * q, 0, make_uint2(0, 0));
+
+  for (int s = 0; s < T_; ++s) {
+    const int t = Rc.dir ? T_ - 1 - s : s;
+#pragma unroll 1
+    for (int blk = 0; blk < NB; ++blk) {
+      uint2 gx[MI][UG][3];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const uint32_t og = ok[i] ? (uint32_t)((rl[i] * T_ + t) * (int)a.ldg + blk * 64 + ub) * 2u : 0x80000000u;
+#pragma unroll
+        for (int u = 0; u < UG; ++u)
+#pragma unroll
+          for (int g = 0; g < 3; ++g) gx[i][u][g] = ld8_buf(rG, og, (g * H + 16 * u) * 2);
+      }
+      float4 bn[UG];
+#pragma unroll
+      for (int u = 0; u < UG; ++u) bn[u] = *reinterpret_cast<const float4*>(Rc.bhn + blk * 64 + ub + 16 * u);
+      f32x4 acc[MI][3 * UG];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < 3 * UG; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#define TT_KS(j, X, Y) rr_kstep<H, NT, WN, D>(rW, w, blk * NK + kt + j, kt + j, s > 0, hb, bst, wm, wn, acc, X, Y)
+      if constexpr (D == 2) {
+#pragma unroll
+        for (int kt = 0; kt < NK; kt += 2) { TT_KS(0, r1, r0); TT_KS(1, r0, r1); }
+      } else {
+#pragma unroll
+        for (int kt = 0; kt < NK; kt += 4) { TT_KS(0, r1, r0); TT_KS(1, r2, r1); TT_KS(2, r3, r2); TT_KS(3, r0, r3); }
+      }
+#undef TT_KS
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int lrow = rl[i] * T_ + t;
+        const uint32_t drow = Rc.row0 + (uint32_t)((long)(m0 + rl[i]) * T_ + t);
+#pragma unroll
+        for (int u = 0; u < UG; ++u) {
+          const int j = blk * 64 + ub + 16 * u;
+          float xr[4], xz[4], xn[4];
+          unpack4(gx[i][u][0], xr);
+          unpack4(gx[i][u][1], xz);
+          unpack4(gx[i][u][2], xn);
+          const float bnv[4] = {bn[u].x, bn[u].y, bn[u].z, bn[u].w};
+          float y[4], sr[4], sz[4], sn[4], sg[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float ghn = acc[i][3 * u + 2][e] + bnv[e];
+            const float ar = xr[e] + acc[i][3 * u][e], az = xz[e] + acc[i][3 * u + 1][e];
+            const float rg = tt_sigmoid(ar), zg = tt_sigmoid(az);
+            const float an = xn[e] + rg * ghn;
+            const float ng = tt_tanh(an);
+            y[e] = (1.f - zg) * ng + zg * hreg[i][0][u][e];
+            sr[e] = ar; sz[e] = az; sn[e] = an; sg[e] = ghn;
+          }
+          const uint32_t oy = ok[i] ? (uint32_t)(lrow * (int)a.ldy + j) * 2u : 0x80000000u;
+          const uint32_t os = ok[i] ? (uint32_t)(lrow * 4 * H + j) * 2u : 0x80000000u;
+#if RR_DBG & 1
+          if (a.B < 0) {  // never: stores off, data kept live
+#endif
+          st8_buf(rY, oy, 0, pack4bf(y));
+          st8_buf(rS, os, 0, pack4bf(sr));
+          st8_buf(rS, os, 2 * H, pack4bf(sz));
+          st8_buf(rS, os, 4 * H, pack4bf(sn));
+          st8_buf(rS, os, 6 * H, pack4bf(sg));
+          if (X1 && a.drop_thresh) {
+            float yd[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              yd[e] = y[e] * tt_dropout_scale(Rc.seed, drow, (uint32_t)(Rc.col0 + j + e), a.drop_thresh, a.inv_keep);
+            st8_buf(rX1, oy, 0, pack4bf(yd));
+          } else {
+            st8_buf(rX1, oy, 0, pack4bf(y));
+          }
+#if RR_DBG & 1
+          }
+#endif
+          // the state of block blk moves to the back: hreg[i][0] is always the current block
+#pragma unroll
+          for (int k = 0; k < NB - 1; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) hreg[i][k][u][e] = hreg[i][k + 1][u][e];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) hreg[i][NB - 1][u][e] = y[e];
+        }
+      }
+    }
+    // h_s -> A operand of step s+1 (every wave finished reading h_{s-1}: the last K-tile
+    // ended with a barrier); unit blk*64 + v is chunk v/8 of K-tile blk, half v&4
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int k = 0; k < NB; ++k)
+#pragma unroll
+        for (int u = 0; u < UG; ++u) {
+          const int v = ub + 16 * u;
+          *reinterpret_cast<uint2*>(hb + k * (R * ttg::KTB) + ttg::kc_off(rl[i], v >> 3) + (v & 4) * 2) =
+              pack4bf(hreg[i][k][u]);
+        }
+    __syncthreads();
+  }
+}
+
 #ifdef TT_DIAG
 }  // namespace
 extern "C" int tt_diag_fwd_prof(unsigned long long* out) {  // [2048][8] host buffer
@@ -1345,8 +1640,19 @@ extern "C" int tt_diag_fwd_prof(unsigned long long* out) {  // [2048][8] host bu
 }
 namespace {
 #endif
+// gru_fwd_rr (experiment) where it applies: bf16, H 512, option gru_fwd_rr 1 (2 x 4 waves),
+// 2 (8 x 1 waves) or 3 (256 threads, one wave per SIMD)
+bool gru_fwd_rr_ok(int dtype, int H) {
+  return dtype == TT_DT_BF16 && H == 512 && tt::opt(tt::OPT_GRU_STEP) != 1 &&
+         tt::opt(tt::OPT_GRU_FWD_RR) != 0;
+}
 bool gru_fwd_persistent(int dtype, int H) {
-  if (dtype != TT_DT_BF16 || H % 64 != 0 || H > PH_MAX) return false;
+  if (gru_fwd_rr_ok(dtype, H)) return true;
+  // only the compile-time-NKT instances (H 256 / 512): the runtime-NKT ones (other H <= 512)
+  // intermittently wrote garbage into the saved gh_n of step 0 (H 64: 33 of 150 runs of
+  // tools/diag_bf16_flake.py, always lanes 12-15 of a 16-lane group; the per-step forward
+  // 0 of 75 on the same box; cause not found), so those widths run per step
+  if (dtype != TT_DT_BF16 || (H != 256 && H != 512)) return false;
   return tt::opt(tt::OPT_GRU_STEP) != 1;
 }
 
@@ -1413,15 +1719,25 @@ extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B
   if (const char* e = getenv("TT_GRU_DBG")) a.dbg = atoi(e);
 #endif
   hipStream_t st = (hipStream_t)stream;
+  if (gru_fwd_rr_ok(dtype, H)) {
+    const dim3 grid(tt_ceil_div(B, 65536 / H) * nrec);
+    const int v = tt::opt(tt::OPT_GRU_FWD_RR);
+    if (v == 1) hipLaunchKernelGGL((gru_fwd_rr<512, 512, 4, 2>), grid, dim3(512), 0, st, a);       // 2 x 4 waves
+    else if (v == 2) hipLaunchKernelGGL((gru_fwd_rr<512, 512, 1, 2>), grid, dim3(512), 0, st, a);  // 8 x 1 waves
+    else hipLaunchKernelGGL((gru_fwd_rr<512, 256, 2, 2>), grid, dim3(256), 0, st, a);              // one wave per SIMD
+    TT_CHECK_LAUNCH("gru_fwd_rr");
+    return 0;
+  }
   if (gru_fwd_persistent(dtype, H)) {
     const dim3 grid(tt_ceil_div(B, PR) * nrec);
     int depth = (H / 64) % 4 == 0 ? 4 : (H / 64) % 2 == 0 ? 2 : 1;
     depth = std::min(depth, tt::opt(tt::OPT_GRU_DEPTH));
     if (depth >= 4 && H == 512) hipLaunchKernelGGL((gru_fwd_seq<4, 8>), grid, dim3(PNT), 0, st, a);
-    else if (depth >= 4 && H == 256) hipLaunchKernelGGL((gru_fwd_seq<4, 4>), grid, dim3(PNT), 0, st, a);
-    else if (depth >= 4) hipLaunchKernelGGL((gru_fwd_seq<4, 0>), grid, dim3(PNT), 0, st, a);
-    else if (depth == 2) hipLaunchKernelGGL((gru_fwd_seq<2, 0>), grid, dim3(PNT), 0, st, a);
-    else hipLaunchKernelGGL((gru_fwd_seq<1, 0>), grid, dim3(PNT), 0, st, a);
+    else if (depth >= 4) hipLaunchKernelGGL((gru_fwd_seq<4, 4>), grid, dim3(PNT), 0, st, a);
+    else if (depth == 2 && H == 512) hipLaunchKernelGGL((gru_fwd_seq<2, 8>), grid, dim3(PNT), 0, st, a);
+    else if (depth == 2) hipLaunchKernelGGL((gru_fwd_seq<2, 4>), grid, dim3(PNT), 0, st, a);
+    else if (H == 512) hipLaunchKernelGGL((gru_fwd_seq<1, 8>), grid, dim3(PNT), 0, st, a);
+    else hipLaunchKernelGGL((gru_fwd_seq<1, 4>), grid, dim3(PNT), 0, st, a);
     TT_CHECK_LAUNCH("gru_fwd_seq");
     return 0;
   }

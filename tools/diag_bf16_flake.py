@@ -47,7 +47,7 @@ towers._gru_layer_bwd = _bwd_probe
 
 
 def run(opts):
-    E, h, B, T = 64, 32, 96, 10
+    E, h, B, T = 64, int(os.environ.get("HID", "32")), 96, 10
     torch.manual_seed(1)
     m = tta.EnhancedTwoTowerModel(E, h)
     with torch.no_grad():

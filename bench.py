@@ -9,7 +9,7 @@ gradient all-reduce (N>1) -> Adam. Workload = BASELINE.json configs[2]
 the job is data-parallel with the doc embeddings all-gathered (configs[3] at N=8),
 i.e. weak scaling at 8192 pairs per rank.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]     (N > 1: starts N local ranks itself)
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Rank 0 prints ONE JSON line. `roofline` is measured live with HIP events around the
@@ -174,8 +174,52 @@ def pmc_traffic(region, launches_per_step, args):
             "traffic_source": f"profiles/{os.path.basename(PMC_SUMMARY)} (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE)"}
 
 
+def spawn_local_ranks(n: int) -> int:
+    """`python bench.py --gpus N` without an external launcher: start N fresh rank
+    processes of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their
+    environment, rendezvous on 127.0.0.1) and return the first nonzero exit code. This
+    parent never makes a GPU call, so each child initialises HIP itself; if one rank
+    fails, the others are terminated instead of waiting in a collective."""
+    import signal
+    import socket
+    import subprocess
+    import sys
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in live:
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc if rc >= 0 else 128 - rc
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(spawn_local_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -196,7 +240,7 @@ def main():
     from two_towers_amd import timing
 
     if args.gpus != world:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 through torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world} from the launcher")
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     B, T, h, E, V = args.batch, args.seq, args.hidden, args.emb, args.vocab
     if args.scaling == "strong":
@@ -204,7 +248,10 @@ def main():
             raise SystemExit(f"--scaling strong: global batch {B} not divisible by {world} GPUs")
         B //= world
     torch.manual_seed(1234)  # same weights on every rank
-    model = tta.EnhancedTwoTowerModel(E, h).to(dev).set_compute_dtype(dt).set_process_group(group).train()
+    # gradients summed inside the backward (head + layer-1 bucket overlapping the layer-0
+    # BPTT); allreduce_grads below is then the only other reducer and skips them
+    model = (tta.EnhancedTwoTowerModel(E, h).to(dev).set_compute_dtype(dt)
+             .set_process_group(group, overlap_grad_allreduce=True).train())
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     table = (torch.randn(V, E, device=dev, generator=gen) * 0.1).to(dt)  # Word2Vec-shaped, resident in HBM
     model.set_embedding_table(table)

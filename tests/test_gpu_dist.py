@@ -115,9 +115,11 @@ def _dp_model(z):
     return m.cuda().eval()
 
 
-def _step_rank(rank, world, port, kind, out):
+def _step_rank(rank, world, port, kind, overlap, out):
     """train_enhanced.py:58-63 on this rank's rows: zero_grad, forward, loss (global
-    negative pool), backward, gradient all-reduce, Adam."""
+    negative pool), backward, gradient all-reduce, Adam. overlap: the tower gradients are
+    summed inside the backward (set_process_group(..., overlap_grad_allreduce=True)) and
+    allreduce_grads sums only the rest; otherwise allreduce_grads sums everything."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -127,7 +129,7 @@ def _step_rank(rank, world, port, kind, out):
         n = z["q"].shape[0] // world
         q = torch.from_numpy(z["q"][rank * n:(rank + 1) * n]).cuda()
         d = torch.from_numpy(z["d"][rank * n:(rank + 1) * n]).cuda()
-        m = _dp_model(z)
+        m = _dp_model(z).set_process_group(None, overlap_grad_allreduce=overlap)
         opt = tta.Adam(m.parameters(), lr=1e-3)
         crit = tta.InfoNCELoss() if kind == "infonce" else tta.HardNegativeMarginLoss(k=5, margin=0.2)
         opt.zero_grad()
@@ -144,29 +146,33 @@ def _step_rank(rank, world, port, kind, out):
         torch.distributed.destroy_process_group()
 
 
+@pytest.mark.parametrize("world,overlap", [(2, False), (2, True), (4, True)])
 @pytest.mark.parametrize("kind", ["infonce", "hardneg"])
-def test_two_rank_train_step_matches_reference_global_batch(kind):
-    """a world-2 data-parallel step over the 256 rows of
-    dp_step.npz (128 per rank) reproduces the reference's single-process step on all 256:
-    loss 1e-5 relative, every all-reduced gradient 2e-3 (max-abs over max, the fp32
-    tolerance of the golden tests), weights after Adam within 1 % of lr, and the mined
-    hard negatives of each rank equal the reference's rows."""
+def test_dp_train_step_matches_reference_global_batch(kind, world, overlap):
+    """a data-parallel step over the 256 rows of dp_step.npz
+    (256 / world per rank; world 4 with the hard-negative margin loss is the configs[3]
+    composition: every rank mines its rows against the all-gathered global pool)
+    reproduces the reference's single-process step on all 256: loss 1e-5 relative, every
+    all-reduced gradient 2e-3 (max-abs over max, the fp32 tolerance of the golden tests),
+    weights after Adam within 1 % of lr, and the mined hard negatives of each rank equal
+    the reference's rows. Both gradient reductions: in the backward (overlap) and after."""
     import numpy as np
     z = _dp_golden()
     ctx = mp.get_context("spawn")
     out = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_step_rank, args=(r, 2, port, kind, out)) for r in range(2)]
+    procs = [ctx.Process(target=_step_rank, args=(r, world, port, kind, overlap, out)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
-    for _ in range(2):
-        r = out.get(timeout=120)
+    for _ in range(world):
+        r = out.get(timeout=180)
         res[r[0]] = r[1:]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for r in range(2):
+    n = z["q"].shape[0] // world
+    for r in range(world):
         loss, grads, w1, idx = res[r]
         ref = float(z[f"{kind}.loss"])
         assert abs(loss - ref) <= 1e-5 * abs(ref), (r, loss, ref)
@@ -176,7 +182,7 @@ def test_two_rank_train_step_matches_reference_global_batch(kind):
         for k, w in w1.items():
             assert float(np.abs(w - z[f"{kind}.w1.{k}"]).max()) <= 1e-5, (r, k)
         if idx is not None:
-            assert (idx == z["hardneg.idx"][r * 128:(r + 1) * 128]).all()
+            assert (idx == z["hardneg.idx"][r * n:(r + 1) * n]).all()
 
 
 def _drop_rank(rank, world, port, out):

@@ -1,0 +1,142 @@
+"""The persistent bf16 GRU forward (gru_fwd_seq, one launch per layer) against the
+per-step forward (gru_fwd_step, option gru_step = 1) on every output it writes: the
+layer output Y, the dropout copy X1 and the saved pre-activations S (r, z, n, gh_n).
+
+Round 2 found the persistent kernel intermittently writing garbage into S's gh_n block
+(step 0, lanes 12-15 of a 16-lane group). The cause was a hardware data hazard: a
+16-byte buffer store whose soffset was an SGPR, followed at once by a VALU write of its
+data registers, which LLVM leaves unprotected for that store form (DESIGN.md §3,
+tools/check_store_hazard.py). These tests pin the fix at the bench grid (B 8192, T 64,
+H 512, the four recurrences of configs[2]) and at the runtime-width instances (H 64 ..
+448) that were retired because of it.
+
+Reference: the recurrence of nn.GRU (enhanced_two_tower.py:17-33, called at :51, :57).
+Both kernels run the same MFMA sequence along K and the same fp32 gate expression, so
+every output is expected bit-identical; the fraction of differing elements and the
+largest difference in bf16 ulps are printed.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from two_towers_amd import _lib  # noqa: E402
+from two_towers_amd._lib import GruFwdRec, call, option, stream_ptr  # noqa: E402
+
+DEV = "cuda"
+
+
+def _inputs(ntow, B, T, H, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    G = [torch.randn(B * T, 6 * H, generator=g, device=DEV).to(torch.bfloat16) for _ in range(ntow)]
+    whh = [[(torch.randn(3 * H, H, generator=g, device=DEV) * H ** -0.5).to(torch.bfloat16) for _ in range(2)]
+           for _ in range(ntow)]
+    bhn = [[torch.randn(H, generator=g, device=DEV) * 0.5 for _ in range(2)] for _ in range(ntow)]
+    return G, whh, bhn
+
+
+def _run(ntow, B, T, H, G, whh, bhn, drop_p, step):
+    dt = torch.bfloat16
+    BT = B * T
+    Y = [torch.empty(BT, 2 * H, dtype=dt, device=DEV) for _ in range(ntow)]
+    X1 = [torch.empty(BT, 2 * H, dtype=dt, device=DEV) for _ in range(ntow)] if drop_p > 0 else None
+    S = [[torch.empty(BT, 4 * H, dtype=dt, device=DEV) for _ in range(2)] for _ in range(ntow)]
+    hs = torch.empty(ntow * 2, 2, B, H, dtype=torch.float32, device=DEV)
+    recs = (GruFwdRec * (2 * ntow))()
+    for ti in range(ntow):
+        for d in range(2):
+            r = recs[ti * 2 + d]
+            r.g = G[ti][:, d * 3 * H:].data_ptr()
+            r.whh = whh[ti][d].data_ptr()
+            r.bhn = bhn[ti][d].data_ptr()
+            r.y = Y[ti][:, d * H:].data_ptr()
+            r.x1 = X1[ti][:, d * H:].data_ptr() if X1 is not None else None
+            r.save = S[ti][d].data_ptr()
+            r.hstate = hs[ti * 2 + d].data_ptr()
+            r.dir = d
+            r.drop_seed = 1234 + ti
+            r.drop_col0 = d * H
+            r.drop_row0 = 0
+    with option("gru_step", step):
+        launches = _lib.load().tt_gru_fwd_launches(_lib.DT_BF16, T, H)
+        call("tt_gru_fwd", _lib.DT_BF16, recs, 2 * ntow, B, T, H, 6 * H, 2 * H, drop_p, stream_ptr())
+        torch.cuda.synchronize()
+    return launches, Y, X1, S
+
+
+def _ulps(a, b):
+    """Largest distance in bf16 ulps between two bf16 tensors (same-sign ordering)."""
+    ia = a.view(torch.int16).to(torch.int32)
+    ib = b.view(torch.int16).to(torch.int32)
+    # map sign-magnitude to a monotone integer line
+    ia = torch.where(ia < 0, -(ia & 0x7FFF), ia)
+    ib = torch.where(ib < 0, -(ib & 0x7FFF), ib)
+    return int((ia - ib).abs().max().item())
+
+
+def _compare(name, a, b, stats):
+    ne = int((a.view(torch.int16) != b.view(torch.int16)).sum().item())
+    u = _ulps(a, b) if ne else 0
+    stats.append((name, ne, a.numel(), u))
+    return ne, u
+
+
+def _check_step0_ghn(S, bhn, B, T, H):
+    """At a recurrence's first step h_{-1} = 0, so the saved gh_n = W_hn h + b_hn is
+    exactly bf16(b_hn) in every row: the slot the round-2 corruption hit."""
+    for ti in range(len(S)):
+        for d in range(2):
+            t0 = 0 if d == 0 else T - 1
+            ghn = S[ti][d].view(B, T, 4 * H)[:, t0, 3 * H:]
+            want = bhn[ti][d].to(torch.bfloat16).expand(B, H)
+            bad = int((ghn.view(torch.int16) != want.view(torch.int16)).sum().item())
+            assert bad == 0, f"tower {ti} dir {d}: {bad} corrupted gh_n values at step 0"
+
+
+def _assert_equivalent(outs_p, outs_s, B, T, H, bhn):
+    lp, Yp, X1p, Sp = outs_p
+    ls, Ys, X1s, Ss = outs_s
+    assert lp == 1 and ls == T, (lp, ls)
+    stats = []
+    for ti in range(len(Yp)):
+        _compare(f"Y{ti}", Yp[ti], Ys[ti], stats)
+        if X1p is not None:
+            _compare(f"X1{ti}", X1p[ti], X1s[ti], stats)
+        for d in range(2):
+            for gi, gname in enumerate(("r", "z", "n", "ghn")):
+                _compare(f"S{ti}{d}.{gname}", Sp[ti][d][:, gi * H:(gi + 1) * H], Ss[ti][d][:, gi * H:(gi + 1) * H],
+                         stats)
+    for name, ne, n, u in stats:
+        print(f"{name}: {ne} of {n} differ, max {u} ulp")
+    for ti in range(len(Sp)):
+        for d in range(2):
+            assert torch.isfinite(Sp[ti][d].float()).all()
+            assert float(Sp[ti][d].float().abs().max()) < 1e3
+    _check_step0_ghn(Sp, bhn, B, T, H)
+    _check_step0_ghn(Ss, bhn, B, T, H)
+    bad = [(name, ne, u) for name, ne, n, u in stats if ne]
+    assert not bad, f"persistent vs per-step forward differ: {bad}"
+
+
+def test_bench_grid_persistent_forward_matches_per_step():
+    """configs[2] layer-0 shape: B 8192, T 64, H 512, 2 towers x 2 directions in one
+    launch, dropout 0.1 on the X1 copy: gru_fwd_seq<4,8> vs T launches of gru_fwd_step."""
+    B, T, H, ntow = 8192, 64, 512, 2
+    G, whh, bhn = _inputs(ntow, B, T, H, seed=3)
+    outs_s = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=1)
+    outs_p = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=0)
+    _assert_equivalent(outs_p, outs_s, B, T, H, bhn)
+
+
+@pytest.mark.parametrize("H,depth", [(64, 4), (128, 4), (128, 1), (192, 4), (256, 2), (320, 4), (384, 4), (448, 4),
+                                     (512, 1)])
+def test_runtime_width_persistent_forward_matches_per_step(H, depth):
+    """The runtime-K-tile-count instances (gru_fwd_seq<D,0>: every H % 64 == 0 below 512
+    other than 256) and a fixed one per register-ring depth D (option gru_depth), with a
+    tail workgroup (B = 1000 = 15 x 64 + 40) and dropout on."""
+    B, T, ntow = 1000, 12, 2
+    G, whh, bhn = _inputs(ntow, B, T, H, seed=H + depth)
+    outs_s = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=1)
+    with option("gru_depth", depth):
+        outs_p = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=0)
+    _assert_equivalent(outs_p, outs_s, B, T, H, bhn)

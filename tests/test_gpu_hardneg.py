@@ -174,3 +174,55 @@ def test_margin_bwd_repeated_negatives(B, nd, h, k, lab, hot):
         torch.cuda.synchronize()
         assert (dq.cpu().double() - rq).abs().max() < 1e-6
         assert (ddn.cpu().double() - rd).abs().max() < 1e-5 * float(rd.abs().max()) + 1e-7
+
+
+# ---------------------------------------------------------------- configs[3] per-rank shape
+# 8 ranks x 8192 pairs: every rank mines its 8192 queries against the all-gathered global
+# pool of 65,536 documents, its own positives at columns rank * 8192 + i.
+
+def test_hardneg_configs3_rank_shape_scan_matches_gemm_and_float64():
+    """B_l 8192 x N 65,536 (rank 3 of 8), h 256, normalised bf16 rows: the streamed scan
+    equals the GEMM + split top-k path bit for bit; against float64 (on the GPU) the
+    returned values are the scores of the returned columns (to fp32 MFMA rounding),
+    sorted, distinct, the positive is never returned and no other column scores above
+    the k-th result."""
+    B, nd, h, k, lab = 8192, 65536, 256, 5, 3 * 8192
+    g = torch.Generator().manual_seed(81)
+    q = torch.nn.functional.normalize(torch.randn(B, h, generator=g), dim=1).bfloat16().float()
+    d = torch.nn.functional.normalize(torch.randn(nd, h, generator=g), dim=1).bfloat16().float()
+    si, sv = run_hardneg(q, d, lab, k, torch.bfloat16)
+    with option("hn_gemm", 1):
+        gi, gv = run_hardneg(q, d, lab, k, torch.bfloat16)
+    assert torch.equal(si, gi) and torch.equal(sv, gv)
+    s = q.to(DEV).double() @ d.to(DEV).double().t()
+    rows = torch.arange(B, device=DEV)
+    s[rows, lab + rows] = -1.0
+    gi_d = si.to(DEV)
+    assert not bool((gi_d == (lab + rows)[:, None]).any())
+    got = torch.gather(s, 1, gi_d)
+    assert float((got.cpu() - sv.double()).abs().max()) < 1e-5
+    assert bool((sv[:, :-1] >= sv[:, 1:]).all())
+    assert all(len(set(r)) == k for r in si[:64].tolist())
+    s.scatter_(1, gi_d, -2.0)
+    assert bool((s.max(dim=1).values.cpu() <= sv[:, -1].double() + 1e-5).all())
+
+
+def test_hardneg_configs3_pool_exact_with_ties():
+    """1024 queries x the 65,536-row pool (label offset 5 * 1024), integer-valued rows so
+    every score is exact: indices and values equal a stable float64 sort on the GPU,
+    exact ties (copied documents far apart in the pool) going to the lower column."""
+    B, nd, h, k, lab = 1024, 65536, 256, 5, 5 * 1024
+    g = torch.Generator().manual_seed(82)
+    q = torch.randint(-3, 4, (B, h), generator=g).float()
+    d = torch.randint(-3, 4, (nd, h), generator=g).float()
+    d[60000] = d[17]
+    d[nd - 1] = d[40000]
+    d[33000:33064] = d[100:164]
+    gi, gv = run_hardneg(q, d, lab, k, torch.bfloat16)
+    s = q.to(DEV).double() @ d.to(DEV).double().t()
+    rows = torch.arange(B, device=DEV)
+    s[rows, lab + rows] = -1.0
+    ri = torch.sort(-s, dim=1, stable=True).indices[:, :k]
+    rv = torch.gather(s, 1, ri)
+    assert torch.equal(gi, ri.cpu())
+    assert torch.equal(gv.double(), rv.cpu())

@@ -90,3 +90,50 @@ def test_flash_and_materialised_paths_agree():
     b = run_bwd(q, d, 1 / 0.07, 0.0, 0, 1 / 1024, 0)
     for x, y in zip(a[:2], b[:2]):
         assert float((x - y).abs().max() / y.abs().max()) < 2e-3
+
+
+def test_infonce_configs3_rank_shape_matches_float64():
+    """configs[3] per-rank shape: 8192 local queries scored against the 65,536-row global
+    pool (rank 3 of 8, labels at 3 * 8192 + i), InfoNCE (tau 0.07). Forward: the per-row
+    LSE and loss against float64 (relative 1e-5 / absolute 2e-4 of the bf16-operand
+    scores); backward (fused, no dS): the tolerances stated at the top of this file. The
+    float64 reference runs on the GPU."""
+    B, nd, h, lab0 = 8192, 65536, 256, 3 * 8192
+    gen = torch.Generator().manual_seed(83)
+    q = torch.nn.functional.normalize(torch.randn(B, h, generator=gen), dim=1)
+    d = torch.nn.functional.normalize(torch.randn(nd, h, generator=gen), dim=1)
+    inv_tau, g = 1 / 0.07, 1.0 / B
+    lib = _lib.load()
+    qd, dd = q.to(DEV, BF).contiguous(), d.to(DEV, BF).contiguous()
+    st = torch.cuda.current_stream().cuda_stream
+    lse = torch.empty(B, device=DEV)
+    row = torch.empty(B, device=DEV)
+    wsf = torch.empty(lib.tt_infonce_fwd_ws_size(B, nd), dtype=torch.uint8, device=DEV)
+    call("tt_infonce_fwd", dtype_code(BF), qd.data_ptr(), B, dd.data_ptr(), nd, h, inv_tau, 0.0, lab0,
+         lse.data_ptr(), row.data_ptr(), wsf.data_ptr(), st)
+    gdev = torch.tensor([g], device=DEV)
+    dq = torch.full((B, h), float("nan"), device=DEV)
+    ddn = torch.full((nd, h), float("nan"), device=DEV)
+    ws = torch.empty(lib.tt_infonce_bwd_ws_size(dtype_code(BF), B, nd, h), dtype=torch.uint8, device=DEV)
+    call("tt_infonce_bwd", dtype_code(BF), qd.data_ptr(), B, dd.data_ptr(), nd, h, inv_tau, 0.0, lab0,
+         lse.data_ptr(), gdev.data_ptr(), dq.data_ptr(), ddn.data_ptr(), ws.data_ptr(), st)
+    torch.cuda.synchronize()
+    q64, d64 = qd.double(), dd.double()
+    s = inv_tau * (q64 @ d64.t())
+    rows = torch.arange(B, device=DEV)
+    rlse = torch.logsumexp(s, dim=1)
+    rrow = rlse - s[rows, lab0 + rows]
+    assert float((lse.double() - rlse).abs().max()) <= 1e-5 * float(rlse.abs().max()) + 2e-4
+    assert float((row.double() - rrow).abs().max()) <= 2e-4
+    p = torch.softmax(s, dim=1)
+    del s
+    p[rows, lab0 + rows] -= 1.0
+    p *= g
+    rq = inv_tau * (p @ d64)
+    rd = inv_tau * (p.t() @ q64)
+    del p
+    for got, ref in ((dq, rq), (ddn, rd)):
+        assert torch.isfinite(got).all()
+        err = float((got.double() - ref).abs().max() / ref.abs().max())
+        cos = float((got.double() * ref).sum() / (got.double().norm() * ref.norm()))
+        assert err <= 1.5e-2 and cos >= 0.9999, (err, cos)

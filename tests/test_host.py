@@ -90,6 +90,30 @@ def test_library_exports_every_header_symbol():
     assert lib.tt_version().decode().startswith("tt_hip")
 
 
+def test_library_has_no_unprotected_wide_buffer_stores():
+    """No 16/12-byte buffer store in the built gfx950 code takes its soffset from a
+    register: LLVM inserts no wait states for that form, and a VALU write of the store's
+    data right after it corrupted the persistent GRU forward's saved gh_n in round 2
+    (tools/check_store_hazard.py)."""
+    import importlib.util
+    from two_towers_amd import _lib
+    if not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"):
+        pytest.skip("llvm-objdump not available")
+    spec = importlib.util.spec_from_file_location("chk", os.path.join(ROOT, "tools", "check_store_hazard.py"))
+    chk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(chk)
+    text = chk.disassemble(_lib.LIB_PATH)
+    assert "gru_fwd_seq" in text and "buffer_store_dwordx4" in text
+    reg_soff, hazards = chk.scan(text)
+    assert not hazards, hazards[:3]
+    assert not reg_soff, reg_soff[:3]
+    # the scanner itself flags the round-2 sequence
+    old = ("_Z3fooPv:\n\tbuffer_store_dwordx4 v[0:3], v158, s[40:43], s61 offen\n"
+           "\tv_mov_b32_e32 v0, v22\n")
+    r, h = chk.scan(old)
+    assert len(r) == 1 and len(h) == 1
+
+
 def test_bad_arguments_are_reported_not_launched():
     from two_towers_amd import _lib
     lib = _lib.load()

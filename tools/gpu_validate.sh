@@ -1,6 +1,6 @@
 #!/bin/bash
 # Full validation on one GPU box: every -m gpu test, smoke, a 2-rank gloo rehearsal of
-# bench.py (the N>1 path incl. the overlapped gradient all-reduce), the bench line and a
+# bench.py started without a launcher (the N>1 path incl. the overlapped gradient all-reduce), the bench line and a
 # rocprofv3 kernel-stats pass. Usage: tools/gpu_validate.sh TAG
 set -o pipefail
 TAG=${1:-v}
@@ -13,8 +13,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider -rf --
 rc=$?; echo "pytest exit=$rc" >> $OUT/pytest_$TAG.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest abnormal exit $rc"; exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1 || { echo smoke failed; exit 3; }
-TT_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-  --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --batch 2048 \
+TT_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --steps 3 --warmup 1 --batch 2048 \
   > $OUT/bench_gloo2_$TAG.json 2> $OUT/bench_gloo2_$TAG.err || { echo gloo rehearsal failed; exit 4; }
 timeout -k 10 600 python bench.py --timing > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { echo bench failed; exit 5; }
 cd /tmp && export TMPDIR=/tmp

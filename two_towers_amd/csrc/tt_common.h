@@ -76,13 +76,19 @@ TT_DEV uint4 pack8bf(const float (&f)[8]) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 // 16-byte buffer store (default cache policy); an offset past num_records is dropped.
+// The soffset field is always the constant 0 and `soff` is folded into the per-lane
+// offset: a wide (> 8-byte) buffer store whose soffset is an SGPR gets no hazard
+// protection from the compiler (LLVM's GCNHazardRecognizer exempts that form), and
+// on gfx950 a VALU write of the data VGPRs right after such a store replaced part of
+// the stored data — the round-2 saved-gh_n corruption (DESIGN.md §3;
+// tools/check_store_hazard.py checks the built library for the form).
 TT_DEV void st16_buf(__amdgpu_buffer_rsrc_t r, uint32_t voff, int soff, uint4 v) {
   tt_u32x4 w = {v.x, v.y, v.z, v.w};
-  __builtin_amdgcn_raw_buffer_store_b128(w, r, (int)voff, soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, (int)(voff + (uint32_t)soff), 0, 0);
 }
 TT_DEV void st16_buf_sc1(__amdgpu_buffer_rsrc_t r, uint32_t voff, int soff, uint4 v) {
   tt_u32x4 w = {v.x, v.y, v.z, v.w};
-  __builtin_amdgcn_raw_buffer_store_b128(w, r, (int)voff, soff, 16);
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, (int)(voff + (uint32_t)soff), 0, 16);
 }
 // Buffer resource of num_records 0x7fffffff bytes, or 0 (every load reads zero) if !on.
 TT_DEV __amdgpu_buffer_rsrc_t tt_rsrc_n(const void* base, bool on) {

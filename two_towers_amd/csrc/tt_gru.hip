@@ -1648,11 +1648,11 @@ bool gru_fwd_rr_ok(int dtype, int H) {
 }
 bool gru_fwd_persistent(int dtype, int H) {
   if (gru_fwd_rr_ok(dtype, H)) return true;
-  // only the compile-time-NKT instances (H 256 / 512): the runtime-NKT ones (other H <= 512)
-  // intermittently wrote garbage into the saved gh_n of step 0 (H 64: 33 of 150 runs of
-  // tools/diag_bf16_flake.py, always lanes 12-15 of a 16-lane group; the per-step forward
-  // 0 of 75 on the same box; cause not found), so those widths run per step
-  if (dtype != TT_DT_BF16 || (H != 256 && H != 512)) return false;
+  // Every bf16 width H % 64 == 0, H <= 512. Round 2 retired the runtime-NKT instances
+  // (H 64: garbage in the saved gh_n of step 0, 33 of 150 probe runs); the cause was the
+  // unprotected wide-store data hazard of SGPR-soffset buffer stores (tt_common.h
+  // st16_buf), which the fixed-NKT bench instances had as well.
+  if (dtype != TT_DT_BF16 || H % 64 != 0 || H > PH_MAX) return false;
   return tt::opt(tt::OPT_GRU_STEP) != 1;
 }
 
@@ -1733,11 +1733,14 @@ extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B
     int depth = (H / 64) % 4 == 0 ? 4 : (H / 64) % 2 == 0 ? 2 : 1;
     depth = std::min(depth, tt::opt(tt::OPT_GRU_DEPTH));
     if (depth >= 4 && H == 512) hipLaunchKernelGGL((gru_fwd_seq<4, 8>), grid, dim3(PNT), 0, st, a);
-    else if (depth >= 4) hipLaunchKernelGGL((gru_fwd_seq<4, 4>), grid, dim3(PNT), 0, st, a);
+    else if (depth >= 4 && H == 256) hipLaunchKernelGGL((gru_fwd_seq<4, 4>), grid, dim3(PNT), 0, st, a);
+    else if (depth >= 4) hipLaunchKernelGGL((gru_fwd_seq<4, 0>), grid, dim3(PNT), 0, st, a);
     else if (depth == 2 && H == 512) hipLaunchKernelGGL((gru_fwd_seq<2, 8>), grid, dim3(PNT), 0, st, a);
-    else if (depth == 2) hipLaunchKernelGGL((gru_fwd_seq<2, 4>), grid, dim3(PNT), 0, st, a);
+    else if (depth == 2 && H == 256) hipLaunchKernelGGL((gru_fwd_seq<2, 4>), grid, dim3(PNT), 0, st, a);
+    else if (depth == 2) hipLaunchKernelGGL((gru_fwd_seq<2, 0>), grid, dim3(PNT), 0, st, a);
     else if (H == 512) hipLaunchKernelGGL((gru_fwd_seq<1, 8>), grid, dim3(PNT), 0, st, a);
-    else hipLaunchKernelGGL((gru_fwd_seq<1, 4>), grid, dim3(PNT), 0, st, a);
+    else if (H == 256) hipLaunchKernelGGL((gru_fwd_seq<1, 4>), grid, dim3(PNT), 0, st, a);
+    else hipLaunchKernelGGL((gru_fwd_seq<1, 0>), grid, dim3(PNT), 0, st, a);
     TT_CHECK_LAUNCH("gru_fwd_seq");
     return 0;
   }
@@ -1746,6 +1749,10 @@ extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B
   int bmr = tt::opt(tt::OPT_GRU_FWD_STEP_ROWS);
   if (bmr != 128 && bmr != 256)
     bmr = (long)tt_ceil_div(H, 64) * tt_ceil_div(B, 256) * nrec >= 512 ? 256 : 128;
+  // the step kernel's S / X1 byte offsets are int relative to the tile's first row
+  const long span = (long)T * std::max({4L * H, ldy, ldg}) * esz;
+  if (bmr == 256 && 256L * span >= (1L << 31)) bmr = 128;
+  TT_CHECK_ARG((long)bmr * span < (1L << 31), "tt_gru_fwd: tile byte offsets exceed 2 GiB (B tile %d)", bmr);
   dim3 grid(tt_ceil_div(H, 64) * tt_ceil_div(B, bmr) * nrec);
   for (int s = 0; s < T; ++s) {
     a.s = s;

@@ -147,8 +147,18 @@ class TwoTowerModel(nn.Module):
         self.compute_dtype = torch.float32
         self._table = None
         self._table_src = None
+        self.process_group = None
+        self.overlap_grad_allreduce = False
 
     # ---------------------------------------------------------------- options
+    def set_process_group(self, group, overlap_grad_allreduce: bool = False):
+        """Data-parallel group; as EnhancedTwoTowerModel.set_process_group (the opt-in
+        overlap sums the GRU gradients inside the backward; the shared projection's are
+        left to dist.allreduce_grads)."""
+        self.process_group = group
+        self.overlap_grad_allreduce = overlap_grad_allreduce
+        return self
+
     def set_compute_dtype(self, dtype: torch.dtype):
         """dtype of the GRU towers (fp32 or bf16 storage, fp32 accumulation); the shared
         projection head always runs in fp32."""
@@ -193,7 +203,7 @@ class TwoTowerModel(nn.Module):
             params.extend(getattr(e, n) for n in _GRU_ORDER)
         table = self._device_table(xs[0].device) if xs[0].dtype in (torch.int32, torch.int64) else None
         return run_towers(cfg, table, xs, params, getattr(self, "process_group", None),
-                          getattr(self, "overlap_grad_allreduce", True) and torch.is_grad_enabled())
+                          getattr(self, "overlap_grad_allreduce", False) and torch.is_grad_enabled())
 
     def _project(self, vecs):
         """The shared projection over the row-stacked towers; returns one [B_i, H] per tower."""

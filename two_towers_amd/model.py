@@ -35,7 +35,7 @@ class EnhancedTwoTowerModel(nn.Module):
         self.hidden_dim = hidden_dim
         self.compute_dtype = torch.float32
         self.process_group = None  # data-parallel group (None: the default group when initialised)
-        self.overlap_grad_allreduce = True  # DP: sum gradients across ranks inside the backward
+        self.overlap_grad_allreduce = False  # DP: sum gradients inside the backward (opt-in)
         self._table = None  # not a parameter/buffer: keeps state_dict identical to the reference
 
     # ---------------------------------------------------------------- options
@@ -45,13 +45,17 @@ class EnhancedTwoTowerModel(nn.Module):
         self.compute_dtype = dtype
         return self
 
-    def set_process_group(self, group, overlap_grad_allreduce: bool = True):
+    def set_process_group(self, group, overlap_grad_allreduce: bool = False):
         """Data-parallel group the batch is split over. The dropout masks depend on it:
         rank r's rows draw the masks of global rows r*B .. r*B+B-1, as one process running
-        the whole global batch would (so the ranks never repeat each other's masks). With
-        overlap_grad_allreduce the backward sums the gradients across the group itself,
-        the head + layer-1 bucket overlapping the layer-0 BPTT (dist.OverlapReducer);
-        dist.allreduce_grads then skips them."""
+        the whole global batch would (so the ranks never repeat each other's masks).
+
+        overlap_grad_allreduce (opt-in): the backward sums the gradients across the group
+        itself, the head + layer-1 bucket overlapping the layer-0 BPTT
+        (dist.OverlapReducer), and dist.allreduce_grads then skips them. The backward then
+        contains collectives, so every rank must run it, and no other reducer (DDP, a
+        manual all_reduce) may sum the same gradients again. Off, the gradients stay
+        per-rank and dist.allreduce_grads (or DDP) sums them after the backward."""
         self.process_group = group
         self.overlap_grad_allreduce = overlap_grad_allreduce
         return self

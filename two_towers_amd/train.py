@@ -75,7 +75,7 @@ def main(argv=None):
         model = TwoTowerModel(E, a.hidden_dim)
         lr = 1e-3 if a.lr is None else a.lr
         tau = 0.1 if a.temperature is None else a.temperature
-    model = model.to(dev).set_compute_dtype(dt)
+    model = model.to(dev).set_compute_dtype(dt).set_process_group(group, overlap_grad_allreduce=world > 1)
     model.set_embedding_table(vocab.device_table(dev))
     if a.loss == "infonce":
         crit = InfoNCELoss(temperature=tau, compute_dtype=dt, process_group=group)

@@ -63,7 +63,8 @@ int tt_pack_rows(int dtype, const float* src, long n, int e, int ep, void* out, 
 /* y[i] = (dtype)x[i] (fp32 -> dtype) for n elements. */
 int tt_cast(int dtype, const float* x, long n, void* y, void* stream);
 
-/* out[c] (+)= sum_r x[r*ld + c] over r < rows (x fp32). Bias gradients. */
+/* out[c] (+)= sum_r x[r*ld + c] over r < rows (x fp32). Bias gradients: summed in a
+ * fixed order (no atomics), so results are bit-for-bit reproducible. */
 int tt_colsum(const float* x, long rows, int cols, long ld, float* out, int accumulate, void* stream);
 
 /* ------------------------------------------------------------------------ GEMM */

@@ -38,17 +38,26 @@ __global__ __launch_bounds__(256) void cast_kernel(const float* __restrict__ x, 
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) Elt<T>::st(y + i, x[i]);
 }
 
-// Column sums: grid.x over column blocks of 256, grid.y over row slabs; one fp32
-// atomic per (slab, column).
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ x, long rows, int cols, long ld,
-                                                     long rows_per_slab, float* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
-  const long r0 = (long)blockIdx.y * rows_per_slab;
-  const long r1 = std::min(rows, r0 + rows_per_slab);
+// Column sums in a fixed order, so bias and LayerNorm gradients are bit-for-bit
+// reproducible run to run (no float atomics): one 1024-thread workgroup per 64
+// columns, wave w adds rows w, w+16, w+32, ... of its column (lane), then the 16 wave
+// sums are added in wave order. Callers pass partial-row buffers (a few hundred rows).
+__global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ x, long rows, int cols, long ld,
+                                                      int accumulate, float* __restrict__ out) {
+  __shared__ float red[16][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (long r = r0; r < r1; ++r) s += x[r * ld + c];
-  atomicAdd(out + c, s);
+  if (c < cols)
+    for (long r = wave; r < rows; r += 16) s += x[r * ld + c];
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += red[w][lane];
+    out[c] = accumulate ? out[c] + t : t;
+  }
 }
 
 __global__ __launch_bounds__(256) void sum_kernel(const float* __restrict__ x, long n, float scale,
@@ -108,15 +117,13 @@ extern "C" int tt_cast(int dtype, const float* x, long n, void* y, void* stream)
 
 extern "C" int tt_colsum(const float* x, long rows, int cols, long ld, float* out, int accumulate, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (!accumulate) TT_CHECK_HIP(hipMemsetAsync(out, 0, sizeof(float) * cols, st));
-  if (rows == 0 || cols == 0) return 0;
-  const int cb = tt_ceil_div(cols, 256);
-  // >= 16 rows per slab, <= 256 workgroups: the GRU bias partials (64 rows x 2048
-  // columns) ran on 8 workgroups of 64 serial loads each (19 us per call)
-  long slabs = std::max<long>(1, std::min<long>(rows / 16, std::max(1, 256 / cb)));
-  const long rps = (rows + slabs - 1) / slabs;
-  slabs = (rows + rps - 1) / rps;
-  hipLaunchKernelGGL(colsum_kernel, dim3(cb, (unsigned)slabs), dim3(256), 0, st, x, rows, cols, ld, rps, out);
+  if (cols == 0) return 0;
+  if (rows == 0) {
+    if (!accumulate) TT_CHECK_HIP(hipMemsetAsync(out, 0, sizeof(float) * cols, st));
+    return 0;
+  }
+  hipLaunchKernelGGL(colsum_kernel, dim3(tt_ceil_div(cols, 64)), dim3(1024), 0, st, x, rows, cols, ld, accumulate,
+                     out);
   TT_CHECK_LAUNCH("colsum_kernel");
   return 0;
 }

@@ -11,6 +11,7 @@
 // the same (b, j) in registers and the update needs no data exchange.
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
 
 #include "tt_api.h"
 #include "tt_gemm_core.h"
@@ -1674,21 +1675,29 @@ static bool gru_bwd_persistent(int dtype, int H) {
 }
 extern "C" int tt_gru_bwd_launches(int dtype, int T, int H) { return gru_bwd_persistent(dtype, H) ? 1 : T; }
 
-// Per-device side stream + fork/join events for tt_gru_bwd's second launch chain.
+// Per-device side stream + fork/join events for tt_gru_bwd's second launch chain,
+// created once per device under a mutex (host threads may call on distinct streams).
+// The fork/join events are per device, so two host threads running the backward on the
+// same device at once must not both take the two-chain path (one stream
+// per thread; the default row-owning and 256-tile backwards never use it).
 struct SideStream {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
 };
 static int side_stream(SideStream** out) {
   static SideStream ss[64];
+  static std::mutex mu;
   int dev = 0;
   TT_CHECK_HIP(hipGetDevice(&dev));
   TT_CHECK_ARG(dev >= 0 && dev < 64, "tt_gru_bwd: device %d", dev);
+  std::lock_guard<std::mutex> lock(mu);
   SideStream& x = ss[dev];
   if (!x.s) {
-    TT_CHECK_HIP(hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking));
-    TT_CHECK_HIP(hipEventCreateWithFlags(&x.fork, hipEventDisableTiming));
-    TT_CHECK_HIP(hipEventCreateWithFlags(&x.join, hipEventDisableTiming));
+    SideStream n;
+    TT_CHECK_HIP(hipStreamCreateWithFlags(&n.s, hipStreamNonBlocking));
+    TT_CHECK_HIP(hipEventCreateWithFlags(&n.fork, hipEventDisableTiming));
+    TT_CHECK_HIP(hipEventCreateWithFlags(&n.join, hipEventDisableTiming));
+    x = n;
   }
   *out = &x;
   return 0;

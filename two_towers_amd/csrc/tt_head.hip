@@ -59,8 +59,12 @@ __global__ __launch_bounds__(256) void ln_relu_fwd_kernel(const T* __restrict__ 
 }
 
 // One wave per row; each block covers rows_per_block rows and writes one partial
-// row [3][C] of (dgamma, dbeta, dx-colsum) to part.
-template <typename T>
+// row [NP][C] of (dgamma, dbeta, dx-colsum [, column sum of dout2]) to part: the
+// partial rows are then summed in a fixed order (tt_colsum), so every bias and affine
+// gradient is bit-for-bit reproducible (no float atomics). dout2 [rows, C2] (NP = 4):
+// the output gradient of the head's last Linear, whose column sum is that layer's bias
+// gradient, read in the same pass.
+template <typename T, int NP>
 __global__ __launch_bounds__(256) void ln_relu_bwd_kernel(const float* __restrict__ du, const T* __restrict__ x,
                                                           const float* __restrict__ gam,
                                                           const float* __restrict__ bet,
@@ -68,14 +72,22 @@ __global__ __launch_bounds__(256) void ln_relu_bwd_kernel(const float* __restric
                                                           const float* __restrict__ rstd, long rows, int C,
                                                           int rows_per_block, T* __restrict__ dx,
                                                           float* __restrict__ part, uint32_t drop_seed,
-                                                          uint32_t drop_thresh, float inv_keep) {
-  __shared__ float red[4][3][LN_MAXC * 64];
+                                                          uint32_t drop_thresh, float inv_keep,
+                                                          const float* __restrict__ dout2, int C2) {
+  __shared__ float red[4][NP][LN_MAXC * 64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  float pg[LN_MAXC], pb[LN_MAXC], pd[LN_MAXC];
+  float pg[LN_MAXC], pb[LN_MAXC], pd[LN_MAXC], p2[LN_MAXC];
 #pragma unroll
-  for (int q = 0; q < LN_MAXC; ++q) pg[q] = pb[q] = pd[q] = 0.f;
+  for (int q = 0; q < LN_MAXC; ++q) pg[q] = pb[q] = pd[q] = p2[q] = 0.f;
   const long r0 = (long)blockIdx.x * rows_per_block;
   for (long row = r0 + wave; row < std::min(rows, r0 + rows_per_block); row += 4) {
+    if constexpr (NP == 4) {
+#pragma unroll
+      for (int q = 0; q < LN_MAXC; ++q) {
+        const int c = lane + 64 * q;
+        if (c < C2) p2[q] += dout2[row * C2 + c];
+      }
+    }
     const float mu = mean[row], rs = rstd[row];
     float xh[LN_MAXC], da[LN_MAXC];
     float s1 = 0.f, s2 = 0.f;
@@ -113,11 +125,12 @@ __global__ __launch_bounds__(256) void ln_relu_bwd_kernel(const float* __restric
     red[wave][0][lane + 64 * q] = pg[q];
     red[wave][1][lane + 64 * q] = pb[q];
     red[wave][2][lane + 64 * q] = pd[q];
+    if constexpr (NP == 4) red[wave][NP - 1][lane + 64 * q] = p2[q];
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < 3 * C; e += 256) {
+  for (int e = threadIdx.x; e < NP * C; e += 256) {
     const int k = e / C, c = e % C;
-    part[(long)blockIdx.x * 3 * C + e] = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
+    part[(long)blockIdx.x * NP * C + e] = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
   }
 }
 
@@ -132,7 +145,7 @@ inline long head_ws_layout(int dtype, int B, int h, long* o_dout, long* o_du, lo
   *o_du = off;   off = al(off + (long)B * 2 * h * 4);
   *o_dp1 = off;  off = al(off + (long)B * 2 * h * esz);
   const long nblk = tt_ceil_div(B, LN_ROWS_PER_BLOCK);
-  *o_part = off; off = al(off + nblk * 3L * 2 * h * 4);
+  *o_part = off; off = al(off + nblk * 4L * 2 * h * 4);
   const int s2 = tt_gemm_pick_splits(h, 2 * h, B, 1);
   const int s1 = tt_gemm_pick_splits(2 * h, 4 * h, B, 1);
   const long sk = std::max(tt_gemm_ws_size(h, 2 * h, 1, s2), tt_gemm_ws_size(2 * h, 4 * h, 1, s1));
@@ -204,24 +217,26 @@ extern "C" int tt_proj_head_bwd(int dtype, const tt_head_bwd_io* io, int ntower,
       const int sp = tt_gemm_pick_splits(h, C, B, 1);
       TT_PROPAGATE(tt_gemm(dtype, TT_DT_F32, 1, 1, h, C, B, &g, 1, h, C, C, 1.f, 0, 0, 0, 0, 0.f, sp, sk, stream));
     }
-    TT_PROPAGATE(tt_colsum(q.dout, B, h, h, q.db2, 0, stream));
     // du = dout w2   [B, 2h]
     {
       tt_gemm_batch g{};
       g.a[0] = dout_t; g.b[0] = q.w2; g.c[0] = du;
       TT_PROPAGATE(tt_gemm(dtype, TT_DT_F32, 0, 1, B, C, h, &g, 1, h, C, C, 1.f, 0, 0, 0, 0, 0.f, 1, nullptr, stream));
     }
-    // LayerNorm + ReLU backward -> dp1, partial (dgamma, dbeta, db1)
+    // LayerNorm + ReLU backward -> dp1, partial (dgamma, dbeta, db1, db2)
     if (dtype == TT_DT_BF16)
-      hipLaunchKernelGGL(ln_relu_bwd_kernel<bf16_t>, dim3(nblk), dim3(256), 0, st, du, (const bf16_t*)q.p1, q.ln_g,
-                         q.ln_b, q.mean, q.rstd, (long)B, C, LN_ROWS_PER_BLOCK, (bf16_t*)dp1, part, 0u, 0u, 1.f);
+      hipLaunchKernelGGL((ln_relu_bwd_kernel<bf16_t, 4>), dim3(nblk), dim3(256), 0, st, du, (const bf16_t*)q.p1,
+                         q.ln_g, q.ln_b, q.mean, q.rstd, (long)B, C, LN_ROWS_PER_BLOCK, (bf16_t*)dp1, part, 0u, 0u,
+                         1.f, q.dout, h);
     else
-      hipLaunchKernelGGL(ln_relu_bwd_kernel<float>, dim3(nblk), dim3(256), 0, st, du, (const float*)q.p1, q.ln_g,
-                         q.ln_b, q.mean, q.rstd, (long)B, C, LN_ROWS_PER_BLOCK, (float*)dp1, part, 0u, 0u, 1.f);
+      hipLaunchKernelGGL((ln_relu_bwd_kernel<float, 4>), dim3(nblk), dim3(256), 0, st, du, (const float*)q.p1,
+                         q.ln_g, q.ln_b, q.mean, q.rstd, (long)B, C, LN_ROWS_PER_BLOCK, (float*)dp1, part, 0u, 0u,
+                         1.f, q.dout, h);
     TT_CHECK_LAUNCH("ln_relu_bwd_kernel");
-    TT_PROPAGATE(tt_colsum(part, nblk, C, 3L * C, q.dg, 0, stream));
-    TT_PROPAGATE(tt_colsum(part + C, nblk, C, 3L * C, q.dbeta, 0, stream));
-    TT_PROPAGATE(tt_colsum(part + 2 * C, nblk, C, 3L * C, q.db1, 0, stream));
+    TT_PROPAGATE(tt_colsum(part, nblk, C, 4L * C, q.dg, 0, stream));
+    TT_PROPAGATE(tt_colsum(part + C, nblk, C, 4L * C, q.dbeta, 0, stream));
+    TT_PROPAGATE(tt_colsum(part + 2 * C, nblk, C, 4L * C, q.db1, 0, stream));
+    TT_PROPAGATE(tt_colsum(part + 3 * C, nblk, h, 4L * C, q.db2, 0, stream));
     // dW1 = dp1^T x   [2h, 4h]
     {
       tt_gemm_batch g{};
@@ -312,13 +327,13 @@ extern "C" int tt_proj_head1_bwd(int dtype, const tt_head1_bwd_io* io, long rows
   const long nblk = tt_ceil_div(rows, LN_ROWS_PER_BLOCK);
   // Dropout + ReLU + LayerNorm backward -> dp1, partial (dgamma, dbeta, db1)
   if (dtype == TT_DT_BF16)
-    hipLaunchKernelGGL(ln_relu_bwd_kernel<bf16_t>, dim3(nblk), dim3(256), 0, st, io->dout, (const bf16_t*)io->p1,
-                       io->ln_g, io->ln_b, io->mean, io->rstd, rows, C, LN_ROWS_PER_BLOCK, (bf16_t*)dp1, part,
-                       drop_seed, thresh, inv_keep);
+    hipLaunchKernelGGL((ln_relu_bwd_kernel<bf16_t, 3>), dim3(nblk), dim3(256), 0, st, io->dout,
+                       (const bf16_t*)io->p1, io->ln_g, io->ln_b, io->mean, io->rstd, rows, C, LN_ROWS_PER_BLOCK,
+                       (bf16_t*)dp1, part, drop_seed, thresh, inv_keep, (const float*)nullptr, 0);
   else
-    hipLaunchKernelGGL(ln_relu_bwd_kernel<float>, dim3(nblk), dim3(256), 0, st, io->dout, (const float*)io->p1,
-                       io->ln_g, io->ln_b, io->mean, io->rstd, rows, C, LN_ROWS_PER_BLOCK, (float*)dp1, part,
-                       drop_seed, thresh, inv_keep);
+    hipLaunchKernelGGL((ln_relu_bwd_kernel<float, 3>), dim3(nblk), dim3(256), 0, st, io->dout,
+                       (const float*)io->p1, io->ln_g, io->ln_b, io->mean, io->rstd, rows, C, LN_ROWS_PER_BLOCK,
+                       (float*)dp1, part, drop_seed, thresh, inv_keep, (const float*)nullptr, 0);
   TT_CHECK_LAUNCH("ln_relu_bwd_kernel");
   TT_PROPAGATE(tt_colsum(part, nblk, C, 3L * C, io->dg, 0, stream));
   TT_PROPAGATE(tt_colsum(part + C, nblk, C, 3L * C, io->dbeta, 0, stream));

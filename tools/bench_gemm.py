@@ -57,8 +57,28 @@ if __name__ == "__main__":
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--regstage", default="", help="TT_GEMM_REGSTAGE value (9 = no epilogue, timing only)")
     ap.add_argument("--lda-pad", type=int, default=0, help="A row stride in elements (K-contig A); -1: lda 0, one row")
+    ap.add_argument("--variants", default="", help="';'-separated option sets, each 'name=v,name=v' (tt_set_option); "
+                                                   "'-' = defaults; rounds interleave the variants")
+    ap.add_argument("--rounds", type=int, default=1)
     a = ap.parse_args()
     if a.regstage:
         os.environ["TT_GEMM_REGSTAGE"] = a.regstage
-    for nm in a.shapes.split(","):
-        print(json.dumps(run(nm, a.iters, a.lda_pad)), flush=True)
+    if not a.variants:
+        for nm in a.shapes.split(","):
+            print(json.dumps(run(nm, a.iters, a.lda_pad)), flush=True)
+    else:
+        from two_towers_amd._lib import get_option, set_option
+        sets = [v for v in a.variants.split(";") if v]
+        names = sorted({kv.split("=")[0] for v in sets if v != "-" for kv in v.split(",")})
+        dflt = {n: get_option(n) for n in names}
+        for rnd in range(a.rounds):
+            for v in sets:
+                opts = dict(dflt)
+                if v != "-":
+                    opts.update({kv.split("=")[0]: int(kv.split("=")[1]) for kv in v.split(",")})
+                for n, x in opts.items():
+                    set_option(n, x)
+                for nm in a.shapes.split(","):
+                    r = run(nm, a.iters, a.lda_pad)
+                    r.update(variant=v, round=rnd)
+                    print(json.dumps(r), flush=True)

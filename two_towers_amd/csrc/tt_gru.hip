@@ -1083,8 +1083,8 @@ TT_DEV void fwd_store_b(char* img, const WTile& r) {
 __device__ unsigned long long g_fwd_prof[2048][8];
 #define TT_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define TT_ACC(i, d) (prf[i] += (d))
-#define TT_PROF_PARAM , unsigned long long (&prf)[8]
-#define TT_PROF_ARGS , prf
+#define TT_PROF_PARAM , unsigned long long (&prf)[8], int dbg
+#define TT_PROF_ARGS , prf, a.dbg
 #else
 #define TT_STAMP(v) do { } while (0)
 #define TT_ACC(i, d) do { } while (0)
@@ -1095,7 +1095,12 @@ template <int D>
 TT_DEV void fwd_kstep(const bf16_t* W, int H, int Q, int q, int kt, bool mm, const char* hb, char* bst, int& it,
                       int wm, int wn, f32x4 (&acc)[2][3], WTile& X, WTile& Y TT_PROF_PARAM) {
   TT_STAMP(t0);
+#ifdef TT_DIAG
+  if (!(dbg & 16)) fwd_load_b(W, H, (q + D) % Q, Y);  // 16: no W_hh loads
+  if (dbg & 8) mm = false;                            // 8: no MFMAs
+#else
   fwd_load_b(W, H, (q + D) % Q, Y);
+#endif
   if (mm) {  // h_{-1} = 0: the first step has no recurrent term
     const char* ia = hb + kt * (PR * ttg::KTB);
     const char* ib = bst + (it & 1) * P_BST;
@@ -1269,9 +1274,20 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
         for (int e = 0; e < 8; ++e) {
           const float ghn = ln[e] + bn[e];
           const float ar = xr[e] + lr[e], az = xz[e] + lz[e];
+#ifdef TT_DIAG
+          float rg, zg, ng, an;
+          if (a.dbg & 4) {  // 4: no transcendentals (cheap stand-ins keep the data flow)
+            rg = ar * 0.25f + 0.5f; zg = az * 0.25f + 0.5f;
+            an = xn[e] + rg * ghn; ng = an * 0.5f;
+          } else {
+            rg = tt_sigmoid(ar); zg = tt_sigmoid(az);
+            an = xn[e] + rg * ghn; ng = tt_tanh(an);
+          }
+#else
           const float rg = tt_sigmoid(ar), zg = tt_sigmoid(az);
           const float an = xn[e] + rg * ghn;
           const float ng = tt_tanh(an);
+#endif
           y[e] = (1.f - zg) * ng + zg * hreg[0][e];
           sr[e] = ar; sz[e] = az; sn[e] = an; sg[e] = ghn;
         }
@@ -1286,7 +1302,11 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
           st16_buf(rS, os, 2 * H, pack8bf(sz));
           st16_buf(rS, os, 4 * H, pack8bf(sn));
           st16_buf(rS, os, 6 * H, pack8bf(sg));
+#ifdef TT_DIAG
+          if (X1 && a.drop_thresh && !(a.dbg & 32)) {  // 32: X1 copy without the mask hash
+#else
           if (X1 && a.drop_thresh) {
+#endif
 #pragma unroll
             for (int e = 0; e < 8; ++e)
               y[e] *= tt_dropout_scale(R.seed, R.row0 + (uint32_t)row, (uint32_t)(R.col0 + j + e), a.drop_thresh,

@@ -140,3 +140,17 @@ def test_runtime_width_persistent_forward_matches_per_step(H, depth):
     with option("gru_depth", depth):
         outs_p = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=0)
     _assert_equivalent(outs_p, outs_s, B, T, H, bhn)
+
+
+@pytest.mark.parametrize("H,B,T", [(512, 8192, 64), (512, 1000, 12), (256, 1000, 12), (512, 70, 3), (256, 64, 1)])
+def test_wave_owned_rows_forward_matches_per_step(H, B, T):
+    """gru_fwd_wr (option gru_fwd_wr = 1: each wave keeps 16 rows' h in registers, W_hh
+    through an LDS-DMA ring with hand-counted vmcnt waits): same MFMA k order and gate
+    arithmetic as the per-step kernel, so every output is bit-identical -- at the bench
+    grid, with a tail workgroup (B 1000 = 15 x 64 + 40; B 70), and at T = 1."""
+    ntow = 2
+    G, whh, bhn = _inputs(ntow, B, T, H, seed=H + B + T)
+    outs_s = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=1)
+    with option("gru_fwd_wr", 1):
+        outs_p = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=0)
+    _assert_equivalent(outs_p, outs_s, B, T, H, bhn)

@@ -1,6 +1,5 @@
 set -o pipefail
-timeout -k 10 500 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_bench_path.py tests/test_gpu_dist.py tests/test_gpu_golden.py -v --timeout 200 --timeout-method thread -p no:cacheprovider -rf > gpurun_out/pt_c.log 2>&1; rc=$?; echo "pytest rc=$rc" >> gpurun_out/pt_c.log
-if [ $rc -gt 1 ]; then exit $rc; fi
-timeout -k 10 300 python tools/diag_bench_path.py > gpurun_out/diag_bp.log 2>&1 || exit 3
-timeout -k 10 300 python bench.py --timing --no-cpu-baseline > gpurun_out/bench_c.json 2> gpurun_out/bench_c.err || exit 4
-tail -2 gpurun_out/pt_c.log
+mkdir -p gpurun_out
+timeout -k 10 600 python tools/bench_gemm.py --shapes input_proj_l0,input_proj_l1,dgrad_l1 --iters 5 --rounds 2 \
+  --variants "-;gemm_persist=0;gemm_persist=0,gemm_regstage=2;gemm_stream_out=0;gemm_a3=0" > gpurun_out/gemm_var_c.log 2>&1
+echo done

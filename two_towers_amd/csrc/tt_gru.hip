@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <mutex>
+#include <type_traits>
 
 #include "tt_api.h"
 #include "tt_gemm_core.h"
@@ -1654,6 +1655,277 @@ __global__ __launch_bounds__(NT) void gru_fwd_rr(FwdArgs a) {
   }
 }
 
+
+// ---- wave-owned-rows persistent forward (gru_fwd_wr, bf16, H 256 / 512) ------------------
+// Each of the 4 waves (one per SIMD) owns 16 batch rows of one recurrence for all T steps
+// and keeps, in its own registers, h_{s-1} as the MFMA operand (bf16, k-step kk = units
+// 32kk .. 32kk+31) and the fp32 state h (for the z * h term). So no hidden state touches LDS:
+// the whole 160 KiB is a 6-slot ring of W_hh K-tiles (192 gate rows x 64 deep = 24 KiB)
+// filled by LDS-DMA five K-tiles ahead, with counted vmcnt waits placed here (every global
+// access of the kernel is inline asm, so hipcc inserts none) and one barrier per K-tile.
+// The W_hh rows of a 64-unit block are permuted inside the K-tile image so that, with the
+// MFMA operands swapped (acc = C^T), a lane's two accumulator fragments of one gate hold 8
+// consecutive units of one batch row: exactly the lane's h operand fragment of k-step
+// 2*blk + cg for the next step, its fp32 state, and one 16-byte G / Y / S / X1 access.
+// Same MFMA sequence along k and the same gate arithmetic as gru_fwd_seq, so the outputs
+// are bit-identical to it and to the per-step kernel.
+// compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N)
+template <int I0, int N, class F>
+TT_DEV void static_for(F&& f) {
+  if constexpr (I0 < N) {
+    f(std::integral_constant<int, I0>{});
+    static_for<I0 + 1, N>(f);
+  }
+}
+
+namespace wr {
+constexpr int NT = 256, NW = 4, ROWS = 64;   // 4 waves x 16 batch rows
+constexpr int TILE = 192 * ttg::KTB;          // W_hh K-tile image: 192 gate rows x 128 B
+constexpr int NSLOT = 6, AHEAD = NSLOT - 1;   // ring slots; K-tiles DMA'd ahead
+constexpr int PPW = TILE / 1024 / NW;         // 1 KiB DMA pieces per wave and K-tile (6)
+constexpr int NGL = 6, NSTO = 12;             // G loads / stores per lane and block
+
+// vmcnt for the wait that retires K-tile kt of a block in steady state: the number of
+// this wave's VMEM operations issued after that K-tile's DMA. Per block, in order:
+// K-tile 0: its DMA (of K-tile +AHEAD), the block's G loads; K-tiles 1..: their DMA;
+// epilogue: the stores.
+constexpr int steady_wait(int nkt, int kt) {
+  // walk back from the current point (before K-tile kt's own DMA) to the DMA of
+  // K-tile (kt - AHEAD), counting everything issued after it
+  int n = 0, b = 0, k = kt;  // position: block offset b (0 = this block), K-tile k
+  for (int back = 0; back < AHEAD; ++back) {
+    // step to the previous K-tile, counting the ops between
+    --k;
+    if (k < 0) { k = nkt - 1; --b; n += NSTO; }  // crossed the previous block's epilogue
+    if (back < AHEAD - 1) n += PPW;              // that K-tile's DMA is younger than ours
+    if (k == 0 && back < AHEAD - 1) n += NGL;    // G loads follow K-tile 0's DMA
+    if (k == 0 && back == AHEAD - 1) n += NGL;   // ... also when K-tile 0 issued our DMA
+  }
+  (void)b;
+  return n;
+}
+}  // namespace wr
+
+TT_DEV uint32_t wr_u32(const void* p, int sh) { return (uint32_t)(((uintptr_t)p) >> sh); }
+// 16-byte buffer load / store from inline asm (invisible to hipcc's vmcnt bookkeeping; the
+// kernel places every wait). The store ends in s_nop 1: a VALU write of its data VGPRs
+// must be two wait states behind it, and hipcc does not see inside the asm.
+TT_DEV tt_u32x4 wr_ld16(tt_u32x4 rs, uint32_t voff) {
+  tt_u32x4 v;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(voff), "s"(rs) : "memory");
+  return v;
+}
+TT_DEV void wr_st16(tt_u32x4 rs, uint32_t voff, uint4 d) {
+  tt_u32x4 v = {d.x, d.y, d.z, d.w};
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs) : "memory");
+}
+// descriptor words as SGPRs (base, num_records 0x7fffffff or 0, default format)
+TT_DEV tt_u32x4 wr_rsrc(const void* base, bool on) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  tt_u32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32) & 0xFFFFu);
+  r[2] = on ? 0x7fffffffu : 0u;
+  r[3] = 0x00020000u;
+  return r;
+}
+template <int N>
+TT_DEV void wr_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// 16 bytes per lane from buffer rs at voff + soff into LDS at lds_addr + 16 * lane (the
+// buffer form of the LDS-DMA: one per-lane 32-bit offset, the per-K-tile offset in soff)
+TT_DEV void wr_dma(tt_u32x4 rs, uint32_t voff, uint32_t soff, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rs), "s"(lds_addr), "s"(soff)
+               : "memory");
+}
+
+template <int H>
+__global__ __launch_bounds__(wr::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gru_fwd_wr(FwdArgs a) {
+  constexpr int KS = H / 32, NB = H / 64, NKT = H / 64;
+  __shared__ __attribute__((aligned(16))) char lds[wr::NSLOT * wr::TILE + H * 4];
+  float* bhn = reinterpret_cast<float*>(lds + wr::NSLOT * wr::TILE);
+  const int ntm = (a.B + wr::ROWS - 1) / wr::ROWS;
+  const int id = ttg::xcd_remap(blockIdx.x, gridDim.x);
+  const int rz = id / ntm;
+  const FwdRec R = a.r[rz];
+  const int T_ = a.T;
+  const int m0 = (id - rz * ntm) * wr::ROWS;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lg = lane >> 4;
+  const int rl = wave * 16 + (lane & 15);  // this lane's batch row within the workgroup
+  const bool rowok = m0 + rl < a.B;
+  const long r0w = (long)m0 * T_;
+  const tt_u32x4 rG = wr_rsrc(static_cast<const bf16_t*>(R.g) + r0w * a.ldg, true);
+  const tt_u32x4 rY = wr_rsrc(static_cast<bf16_t*>(R.y) + r0w * a.ldy, true);
+  const tt_u32x4 rX = wr_rsrc(R.x1 ? static_cast<bf16_t*>(R.x1) + r0w * a.ldy : R.y, R.x1 != nullptr);
+  const tt_u32x4 rS = wr_rsrc(static_cast<bf16_t*>(R.save) + r0w * 4L * H, true);
+  const bool drop = R.x1 != nullptr && a.drop_thresh != 0;
+  for (int i = tid; i < H; i += wr::NT) bhn[i] = R.bhn[i];
+
+  // this lane's DMA pieces: image row ir = 8 p + lane/8 (p = wave*PPW + j), 16-byte
+  // position lane%8 holds chunk c = pos ^ swz(ir) of W_hh row g*H + 64 blk + unit(ir)
+  uint32_t poff[wr::PPW];
+#pragma unroll
+  for (int j = 0; j < wr::PPW; ++j) {
+    const int p = wave * wr::PPW + j, ir = 8 * p + (lane >> 3), pos = lane & 7;
+    const int c = pos ^ ((ir >> 1) & 7);
+    const int f = ir >> 4, rho = ir & 15;
+    const int g = f >> 2, cg = (f >> 1) & 1, pp = f & 1;
+    const int u = 32 * cg + 8 * (rho >> 2) + 4 * pp + (rho & 3);
+    poff[j] = (uint32_t)(((g * H + u) * H + 8 * c) * 2);
+  }
+  tt_u32x4 rW = wr_rsrc(R.whh, true);
+  rW[2] = (uint32_t)(3 * H * H * 2);  // exact size: offsets past it read zeros
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane(ttg::lds_addr_of(lds));
+  // DMA of stream K-tile q (block qb = (q / NKT) % NB, K-tile qk = q % NKT) into its slot;
+  // past the stream's end an out-of-range offset (zeros), so every wave always issues PPW
+  const int QT = (T_ - 1) * NB * NKT;
+  auto dma = [&](int q) __attribute__((always_inline)) {
+    const int qk = q % NKT, qb = (q / NKT) % NB, slot = q % wr::NSLOT;
+    const uint32_t so = q < QT ? (uint32_t)(qb * 64 * H * 2 + qk * ttg::KTB) : 0x40000000u;
+    const uint32_t lb = lbase + (uint32_t)(slot * wr::TILE + wave * wr::PPW * 1024);
+#pragma unroll
+    for (int j = 0; j < wr::PPW; ++j) wr_dma(rW, poff[j], so, lb + (uint32_t)(j * 1024));
+  };
+
+  uint4 hA[KS];       // h_{s-1}, bf16, as the MFMA operand of k-step kk
+  float st[KS][8];    // fp32 state: units 32 kk + 8 lg + e of row rl
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    hA[kk] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) st[kk][e] = 0.f;
+  }
+
+  // G loads of block blk at time t (6 per lane: gates r, z, n of unit groups cg 0 / 1)
+  auto load_g = [&](int blk, int t, tt_u32x4 (&gx)[2][3]) __attribute__((always_inline)) {
+    const uint32_t og = rowok ? (uint32_t)((rl * T_ + t) * (int)a.ldg + 64 * blk + 8 * lg) * 2u : 0x80000000u;
+#pragma unroll
+    for (int cg = 0; cg < 2; ++cg)
+#pragma unroll
+      for (int g = 0; g < 3; ++g) gx[cg][g] = wr_ld16(rG, og + (uint32_t)((g * H + 32 * cg) * 2));
+  };
+  // epilogue of block blk at time t from the accumulators (C^T fragments f = 4g + 2cg + pp)
+  auto epilogue = [&](int blk, int t, const f32x4 (&acc)[12], tt_u32x4 (&gx)[2][3]) __attribute__((always_inline)) {
+    const uint32_t oy = rowok ? (uint32_t)((rl * T_ + t) * (int)a.ldy + 64 * blk + 8 * lg) * 2u : 0x80000000u;
+    const uint32_t os = rowok ? (uint32_t)((rl * T_ + t) * 4 * H + 64 * blk + 8 * lg) * 2u : 0x80000000u;
+    const uint32_t row = R.row0 + (uint32_t)((m0 + rl) * T_ + t);
+#pragma unroll
+    for (int cg = 0; cg < 2; ++cg) {
+      const int kk = 2 * blk + cg;
+      float xr[8], xz[8], xn[8], bn[8], y[8], sr[8], sz[8], sn[8], sg[8];
+      unpack8(make_uint4(gx[cg][0][0], gx[cg][0][1], gx[cg][0][2], gx[cg][0][3]), xr);
+      unpack8(make_uint4(gx[cg][1][0], gx[cg][1][1], gx[cg][1][2], gx[cg][1][3]), xz);
+      unpack8(make_uint4(gx[cg][2][0], gx[cg][2][1], gx[cg][2][2], gx[cg][2][3]), xn);
+      const float4 b0 = *reinterpret_cast<const float4*>(bhn + 64 * blk + 32 * cg + 8 * lg);
+      const float4 b1 = *reinterpret_cast<const float4*>(bhn + 64 * blk + 32 * cg + 8 * lg + 4);
+      bn[0] = b0.x; bn[1] = b0.y; bn[2] = b0.z; bn[3] = b0.w;
+      bn[4] = b1.x; bn[5] = b1.y; bn[6] = b1.z; bn[7] = b1.w;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int pp = e >> 2, r = e & 3;
+        const float ghn = acc[8 + 2 * cg + pp][r] + bn[e];
+        const float ar = xr[e] + acc[2 * cg + pp][r], az = xz[e] + acc[4 + 2 * cg + pp][r];
+        const float rg = tt_sigmoid(ar), zg = tt_sigmoid(az);
+        const float an = xn[e] + rg * ghn;
+        const float ng = tt_tanh(an);
+        y[e] = (1.f - zg) * ng + zg * st[kk][e];
+        st[kk][e] = y[e];
+        sr[e] = ar; sz[e] = az; sn[e] = an; sg[e] = ghn;
+      }
+      const uint32_t dc = (uint32_t)(32 * cg * 2);
+      wr_st16(rY, oy + dc, pack8bf(y));
+      wr_st16(rS, os + dc, pack8bf(sr));
+      wr_st16(rS, os + dc + 2 * H, pack8bf(sz));
+      wr_st16(rS, os + dc + 4 * H, pack8bf(sn));
+      wr_st16(rS, os + dc + 6 * H, pack8bf(sg));
+      if (drop) {
+        // the mask columns are loop-invariant: opaque here, or hipcc hoists all of them out
+        // of the step loop and spills them
+        uint32_t cb = (uint32_t)(R.col0 + 64 * blk + 32 * cg + 8 * lg);
+        asm volatile("" : "+v"(cb));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) y[e] *= tt_dropout_scale(R.seed, row, cb + e, a.drop_thresh, a.inv_keep);
+      }
+      wr_st16(rX, oy + dc, pack8bf(y));
+    }
+  };
+  // one K-tile (64 deep = k-steps 2 kt, 2 kt + 1) of block blk from ring slot q % NSLOT
+  auto ktile = [&](int q, int kt, f32x4 (&acc)[12]) __attribute__((always_inline)) {
+    const char* img = lds + (q % wr::NSLOT) * wr::TILE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 fb[12];
+#pragma unroll
+      for (int f = 0; f < 12; ++f) fb[f] = ttg::frag<bf16_t, false>(img, 16 * f, ks);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int f = 0; f < 12; ++f) acc[f] = ttg::mma<bf16_t>(fb[f], hA[2 * kt + ks], acc[f]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  };
+  __syncthreads();  // bhn staged
+
+  // step 0: h_{-1} = 0, gates from G alone
+  {
+    const int t = R.dir ? T_ - 1 : 0;
+    f32x4 acc[12];
+#pragma unroll
+    for (int f = 0; f < 12; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+    static_for<0, NB>([&](auto bc) __attribute__((always_inline)) {
+      constexpr int blk = decltype(bc)::value;
+      tt_u32x4 gx[2][3];
+      load_g(blk, t, gx);
+      wr_wait<0>();
+      asm volatile("" : "+v"(gx[0][0]), "+v"(gx[0][1]), "+v"(gx[0][2]), "+v"(gx[1][0]), "+v"(gx[1][1]), "+v"(gx[1][2]));
+      epilogue(blk, t, acc, gx);
+    });
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) hA[kk] = pack8bf(st[kk]);
+  }
+  if (T_ == 1) {
+    wr_wait<0>();
+    return;
+  }
+  // the stream: K-tiles of steps 1 .. T-1; prologue DMAs K-tiles 0 .. AHEAD-1
+#pragma unroll
+  for (int q = 0; q < wr::AHEAD; ++q) dma(q);
+  int q = 0;
+  for (int s = 1; s < T_; ++s) {
+    const int t = R.dir ? T_ - 1 - s : s;
+    const bool steady = s >= 2;  // step 1: conservative waits (the prologue's history differs)
+    static_for<0, NB>([&](auto bc) __attribute__((always_inline)) {
+      constexpr int blk = decltype(bc)::value;
+      f32x4 acc[12];
+#pragma unroll
+      for (int f = 0; f < 12; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+      tt_u32x4 gx[2][3];
+      static_for<0, NKT>([&](auto kc) __attribute__((always_inline)) {
+        constexpr int kt = decltype(kc)::value;
+        // K-tile q landed (this wave's pieces), then every wave's
+        if (steady) wr_wait<wr::steady_wait(NKT, kt)>();
+        else wr_wait<wr::PPW * (wr::AHEAD - 1)>();
+        __builtin_amdgcn_s_barrier();
+        dma(q + wr::AHEAD);
+        if constexpr (kt == 0) load_g(blk, t, gx);
+        ktile(q, kt, acc);
+        ++q;
+      });
+      // G of this block: issued after K-tile 0's DMA, followed by NKT-1 K-tiles' DMAs
+      wr_wait<wr::PPW * (NKT - 1)>();
+      asm volatile("" : "+v"(gx[0][0]), "+v"(gx[0][1]), "+v"(gx[0][2]), "+v"(gx[1][0]), "+v"(gx[1][1]), "+v"(gx[1][2]));
+      epilogue(blk, t, acc, gx);
+    });
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) hA[kk] = pack8bf(st[kk]);
+  }
+  wr_wait<0>();  // trailing zero-page DMAs land before the workgroup exits
+  __builtin_amdgcn_s_barrier();
+}
+
 #ifdef TT_DIAG
 }  // namespace
 extern "C" int tt_diag_fwd_prof(unsigned long long* out) {  // [2048][8] host buffer
@@ -1667,8 +1939,12 @@ bool gru_fwd_rr_ok(int dtype, int H) {
   return dtype == TT_DT_BF16 && H == 512 && tt::opt(tt::OPT_GRU_STEP) != 1 &&
          tt::opt(tt::OPT_GRU_FWD_RR) != 0;
 }
+bool gru_fwd_wr_ok(int dtype, int H) {
+  return dtype == TT_DT_BF16 && (H == 256 || H == 512) && tt::opt(tt::OPT_GRU_STEP) != 1 &&
+         tt::opt(tt::OPT_GRU_FWD_WR) != 0 && tt::opt(tt::OPT_GRU_FWD_RR) == 0;
+}
 bool gru_fwd_persistent(int dtype, int H) {
-  if (gru_fwd_rr_ok(dtype, H)) return true;
+  if (gru_fwd_rr_ok(dtype, H) || gru_fwd_wr_ok(dtype, H)) return true;
   // Every bf16 width H % 64 == 0, H <= 512. Round 2 retired the runtime-NKT instances
   // (H 64: garbage in the saved gh_n of step 0, 33 of 150 probe runs); the cause was the
   // unprotected wide-store data hazard of SGPR-soffset buffer stores (tt_common.h
@@ -1755,6 +2031,13 @@ extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B
     else if (v == 2) hipLaunchKernelGGL((gru_fwd_rr<512, 512, 1, 2>), grid, dim3(512), 0, st, a);  // 8 x 1 waves
     else hipLaunchKernelGGL((gru_fwd_rr<512, 256, 2, 2>), grid, dim3(256), 0, st, a);              // one wave per SIMD
     TT_CHECK_LAUNCH("gru_fwd_rr");
+    return 0;
+  }
+  if (gru_fwd_wr_ok(dtype, H)) {
+    const dim3 grid(tt_ceil_div(B, wr::ROWS) * nrec);
+    if (H == 512) hipLaunchKernelGGL(gru_fwd_wr<512>, grid, dim3(wr::NT), 0, st, a);
+    else hipLaunchKernelGGL(gru_fwd_wr<256>, grid, dim3(wr::NT), 0, st, a);
+    TT_CHECK_LAUNCH("gru_fwd_wr");
     return 0;
   }
   if (gru_fwd_persistent(dtype, H)) {

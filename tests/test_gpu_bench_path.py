@@ -216,3 +216,40 @@ def test_bench_composition_hardneg_margin_matches_oracle():
         assert float((a - b).abs().max() / b.abs().max()) <= 3e-2
     frob, c, kname = _grad_check(dict(m.named_parameters()), p)
     print(f"composition: loss {lv:.6f} vs {rv:.6f}; worst gradient {kname}: rel {frob:.4f}, cos {c:.5f}")
+
+
+def test_reference_size_h512_t128_bf16_matches_oracle():
+    """configs[4]'s model and sequence length: hidden_dim 512 (GRU H = 1024,
+    train_enhanced.py:30, enhanced_two_tower.py:19), T = 128, bf16, dropout 0.1, B = 16,
+    InfoNCE + backward, against the fp32 oracle on bf16-rounded operands. Runs the kernels
+    configs[4] runs (per-step bf16 forward, 256 x 256 per-step BPTT) over 128 steps, so the
+    bf16 rounding of the recurrent state, the saved pre-activations and the BPTT carry
+    compounds over twice the steps of the bench configuration; tolerances as stated at the
+    top of this file."""
+    Hd, Tq, Bq = 512, 128, 16
+    torch.manual_seed(38)
+    m = tta.EnhancedTwoTowerModel(E, Hd)
+    with torch.no_grad():
+        for prm in m.parameters():
+            prm.copy_(_bf16(prm))
+    p = {k: v.detach().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    m = m.to(DEV).set_compute_dtype(torch.bfloat16).train()
+    g = torch.Generator().manual_seed(39)
+    q = _bf16(torch.randn(Bq, Tq, E, generator=g) * 0.5)
+    d = _bf16(torch.randn(Bq, Tq, E, generator=g) * 0.5)
+    torch.manual_seed(40)
+    qv, dv = m(q.to(DEV), d.to(DEV))
+    loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
+    loss.backward()
+    torch.manual_seed(40)
+    seeds = [int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) for _ in range(2)]
+    rq, rd = cpu_ref.forward(q, d, p, drop_p=0.1, seeds=seeds)
+    rl = cpu_ref.infonce(rq, rd)
+    rl.backward()
+    lv, rv = float(loss.detach()), float(rl.detach())
+    assert abs(lv - rv) <= 2e-3 * abs(rv), (lv, rv)
+    for a, b in ((qv, rq), (dv, rd)):
+        a, b = a.detach().double().cpu(), b.detach().double()
+        assert float((a - b).abs().max() / b.abs().max()) <= 3e-2
+    frob, cos, k = _grad_check(dict(m.named_parameters()), p)
+    print(f"h 512 T 128: loss {lv:.6f} vs {rv:.6f}; worst gradient {k}: rel {frob:.4f}, cos {cos:.5f}")

@@ -51,6 +51,26 @@ struct BwdArgs {
 #endif
 };
 
+
+// The forward GRU cell (enhanced_two_tower.py:17-33 via nn.GRU) in one fixed operation
+// order, shared by every forward kernel: FP contraction is off and the two fused
+// multiply-adds are explicit, so no kernel's result depends on how hipcc contracted its
+// own copy of the expression -- the per-step, persistent and wave-owned-rows forwards are
+// bit-identical by construction. Returns h' and the saved pre-activations.
+TT_DEV void gru_cell(float xr, float xz, float xn, float lr, float lz, float ln, float bn, float hp, float& y,
+                     float& ar, float& az, float& an, float& ghn) {
+#pragma clang fp contract(off)
+  constexpr float L2E = 0x1.715476p+0f;
+  ghn = ln + bn;
+  ar = xr + lr;
+  az = xz + lz;
+  const float rg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(L2E * -ar));
+  const float zg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(L2E * -az));
+  an = __builtin_fmaf(rg, ghn, xn);
+  const float ng = 1.0f - 2.0f * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(L2E * (2.0f * an)) + 1.0f);
+  y = __builtin_fmaf(zg, hp, (1.0f - zg) * ng);
+}
+
 // B-tile row r of the forward step -> row (gate*H + j) of Whh [3H, H].
 template <typename T>
 struct GateRows {
@@ -145,17 +165,10 @@ __global__ __launch_bounds__(2 * BMR) void gru_fwd_step(FwdArgs a) {
         const float* Lz = L + (1 * 64 + rl) * FLD + jg;
         const float* Ln = L + (2 * 64 + rl) * FLD + jg;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float ghn = Ln[e] + bn[e];
-          const float ar = xr[e] + Lr[e], az = xz[e] + Lz[e];
-          const float rg = tt_sigmoid(ar), zg = tt_sigmoid(az);
-          const float an = xn[e] + rg * ghn;
-          const float ng = tt_tanh(an);
-          y[e] = (1.f - zg) * ng + zg * hp[e];
-          // pre-activations, not gate values: the backward recomputes sigma/tanh in
-          // fp32, so 1-z and 1-n^2 keep full precision even with bf16 storage
-          sr[e] = ar; sz[e] = az; sn[e] = an; sg[e] = ghn;
-        }
+        for (int e = 0; e < 8; ++e)
+          // saved: pre-activations, not gate values: the backward recomputes sigma/tanh
+          // in fp32, so 1-z and 1-n^2 keep full precision even with bf16 storage
+          gru_cell(xr[e], xz[e], xn[e], Lr[e], Lz[e], Ln[e], bn[e], hp[e], y[e], sr[e], sz[e], sn[e], sg[e]);
         st8(hs_cur + (long)b * H + j, y);
         st8(Yw + row * a.ldy + j, y);
         // saved pre-activations and the dropout copy are only read by later kernels:
@@ -1273,24 +1286,17 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
         }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float ghn = ln[e] + bn[e];
-          const float ar = xr[e] + lr[e], az = xz[e] + lz[e];
 #ifdef TT_DIAG
-          float rg, zg, ng, an;
           if (a.dbg & 4) {  // 4: no transcendentals (cheap stand-ins keep the data flow)
-            rg = ar * 0.25f + 0.5f; zg = az * 0.25f + 0.5f;
-            an = xn[e] + rg * ghn; ng = an * 0.5f;
-          } else {
-            rg = tt_sigmoid(ar); zg = tt_sigmoid(az);
-            an = xn[e] + rg * ghn; ng = tt_tanh(an);
+            sg[e] = ln[e] + bn[e];
+            sr[e] = xr[e] + lr[e]; sz[e] = xz[e] + lz[e];
+            const float rg = sr[e] * 0.25f + 0.5f, zg = sz[e] * 0.25f + 0.5f;
+            sn[e] = xn[e] + rg * sg[e];
+            y[e] = (1.f - zg) * sn[e] * 0.5f + zg * hreg[0][e];
+            continue;
           }
-#else
-          const float rg = tt_sigmoid(ar), zg = tt_sigmoid(az);
-          const float an = xn[e] + rg * ghn;
-          const float ng = tt_tanh(an);
 #endif
-          y[e] = (1.f - zg) * ng + zg * hreg[0][e];
-          sr[e] = ar; sz[e] = az; sn[e] = an; sg[e] = ghn;
+          gru_cell(xr[e], xz[e], xn[e], lr[e], lz[e], ln[e], bn[e], hreg[0][e], y[e], sr[e], sz[e], sn[e], sg[e]);
         }
         float ynew[8];
 #pragma unroll
@@ -1598,15 +1604,9 @@ __global__ __launch_bounds__(NT) void gru_fwd_rr(FwdArgs a) {
           const float bnv[4] = {bn[u].x, bn[u].y, bn[u].z, bn[u].w};
           float y[4], sr[4], sz[4], sn[4], sg[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float ghn = acc[i][3 * u + 2][e] + bnv[e];
-            const float ar = xr[e] + acc[i][3 * u][e], az = xz[e] + acc[i][3 * u + 1][e];
-            const float rg = tt_sigmoid(ar), zg = tt_sigmoid(az);
-            const float an = xn[e] + rg * ghn;
-            const float ng = tt_tanh(an);
-            y[e] = (1.f - zg) * ng + zg * hreg[i][0][u][e];
-            sr[e] = ar; sz[e] = az; sn[e] = an; sg[e] = ghn;
-          }
+          for (int e = 0; e < 4; ++e)
+            gru_cell(xr[e], xz[e], xn[e], acc[i][3 * u][e], acc[i][3 * u + 1][e], acc[i][3 * u + 2][e], bnv[e],
+                     hreg[i][0][u][e], y[e], sr[e], sz[e], sn[e], sg[e]);
           const uint32_t oy = ok[i] ? (uint32_t)(lrow * (int)a.ldy + j) * 2u : 0x80000000u;
           const uint32_t os = ok[i] ? (uint32_t)(lrow * 4 * H + j) * 2u : 0x80000000u;
 #if RR_DBG & 1
@@ -1827,14 +1827,9 @@ __global__ __launch_bounds__(wr::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int pp = e >> 2, r = e & 3;
-        const float ghn = acc[8 + 2 * cg + pp][r] + bn[e];
-        const float ar = xr[e] + acc[2 * cg + pp][r], az = xz[e] + acc[4 + 2 * cg + pp][r];
-        const float rg = tt_sigmoid(ar), zg = tt_sigmoid(az);
-        const float an = xn[e] + rg * ghn;
-        const float ng = tt_tanh(an);
-        y[e] = (1.f - zg) * ng + zg * st[kk][e];
+        gru_cell(xr[e], xz[e], xn[e], acc[2 * cg + pp][r], acc[4 + 2 * cg + pp][r], acc[8 + 2 * cg + pp][r], bn[e],
+                 st[kk][e], y[e], sr[e], sz[e], sn[e], sg[e]);
         st[kk][e] = y[e];
-        sr[e] = ar; sz[e] = az; sn[e] = an; sg[e] = ghn;
       }
       const uint32_t dc = (uint32_t)(32 * cg * 2);
       wr_st16(rY, oy + dc, pack8bf(y));

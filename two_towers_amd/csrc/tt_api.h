@@ -31,6 +31,7 @@ enum Opt {
   OPT_INFONCE_FLASH,    // 0: InfoNCE backward through a materialised dS (bf16, h 128/256 default fused)
   OPT_GRU_FWD_RR,       // 1/2/3: experimental 128-row forward with gates in registers (bf16, H 512)
   OPT_GRU_FWD_WR,       // 1: wave-owned-rows persistent forward (bf16, H 256 / 512; h in registers)
+  OPT_HN_MAP,           // hn_scan block -> (row tile, split) map: 0 split per XCD, 1 row tile per XCD
   OPT_N
 };
 int opt(Opt o);

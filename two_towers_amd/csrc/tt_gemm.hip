@@ -35,7 +35,7 @@ constexpr OptDef kOpts[OPT_N] = {
     {"gru_bwd_persist", "TT_GRU_BWD_PERSIST", 1}, {"gru_bwd_r64", "TT_GRU_BWD_R64", 0},
     {"gru_bwd_phase", "TT_GRU_BWD_PHASE", 0},     {"gru_fwd_step_rows", "TT_GRU_FWD_STEP_ROWS", 0},
     {"infonce_flash", "TT_INFONCE_FLASH", 1},     {"gru_fwd_rr", "TT_GRU_FWD_RR", 0},
-    {"gru_fwd_wr", "TT_GRU_FWD_WR", 0},
+    {"gru_fwd_wr", "TT_GRU_FWD_WR", 0},           {"hn_map", "TT_HN_MAP", 0},
 };
 struct OptTable {
   std::atomic<int> v[OPT_N];

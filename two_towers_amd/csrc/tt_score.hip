@@ -102,12 +102,16 @@ template <int KS>
 __global__ __launch_bounds__(SC_WAVES * 64, 1) void hn_scan_kernel(const bf16_t* __restrict__ Q, long bq,
                                                                  const bf16_t* __restrict__ D, long nd,
                                                                  long label_off, int S, int tps, long nch,
-                                                                 float* __restrict__ CM) {
+                                                                 float* __restrict__ CM, int map) {
   using TI = ScanTile<KS>;
   // 4 x 32 KiB tile ring + chunk maxima [tile][row]: all 160 KiB, one workgroup per CU
   __shared__ __attribute__((aligned(16))) char lds[SC_SLOTS * TI::BYTES + SC_TPS_MAX * SC_ROWS * 4];
   float* cms = reinterpret_cast<float*>(lds + SC_SLOTS * TI::BYTES);
-  const int split = blockIdx.x % S, rt = blockIdx.x / S;
+  // map 0: blocks round-robin over the XCDs, so split b % S stays on one XCD and its
+  // document slice in that L2; map 1 (option hn_map): the S splits of a row tile share an
+  // XCD (xcd_remap), so the tile's query rows are fetched into that L2 once
+  const int bid = map ? ttg::xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int split = bid % S, rt = bid / S;
   const long t0 = (long)split * tps;
   const int nt = (int)(nch - t0 < tps ? nch - t0 : tps);
   if (nt <= 0) return;
@@ -419,7 +423,7 @@ int hn_run(const bf16_t* qn, long bq, const bf16_t* dn, long nd, long label_offs
   float* cand = reinterpret_cast<float*>(ws + p.off_cand);
   const int nsel = (int)(p.nch < k ? p.nch : k);
   hipLaunchKernelGGL((hn_scan_kernel<KS>), dim3((unsigned)(p.RT * p.S)), dim3(SC_WAVES * 64), 0, st, qn, bq, dn, nd, label_offset, (int)p.S,
-                     (int)p.tps, p.nch, CM);
+                     (int)p.tps, p.nch, CM, tt::opt(tt::OPT_HN_MAP));
   TT_CHECK_LAUNCH("hn_scan_kernel");
   const dim3 rows4((unsigned)tt_ceil_div(bq, 4));
   if (k <= 8)

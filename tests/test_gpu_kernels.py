@@ -192,3 +192,36 @@ def test_gemm_persistent_tiles(akout, bkout, out, n):
         ref = torch.relu(As[i] @ Bs[i].t() + bias[i])
         tol = 1e-5 if out == torch.float32 else 8e-3
         assert rel_err(C[i].float(), ref) < tol, (i, rel_err(C[i].float(), ref))
+
+
+@pytest.mark.parametrize("stream", [0, 1])
+def test_gemm_persistent_bf16_output_is_rounded_fp32(stream):
+    """The persistent kernel's direct epilogue (transposed accumulators, bf16 pairs
+    exchanged between column tiles by v_permlane16_swap): its bf16 output must be exactly
+    the bf16 rounding of its own fp32 output, element by element, with bias, alpha and
+    dropout applied; stream 1 is large enough (>= 64 MiB of output) for the write-through
+    store form. A wrong lane -> column map moves values between columns and fails here
+    even where a relative-error check could not see it."""
+    from two_towers_amd._lib import option
+    dt = torch.bfloat16
+    m, n, k = (16640, 4352, 136) if stream else (8448, 4352, 200)  # >= 512 tiles
+    g = torch.Generator().manual_seed(11 + stream)
+    A = torch.randn(m, k, generator=g).to(DEV, dt)
+    B = torch.randn(n, k, generator=g).to(DEV, dt)
+    bias = torch.randn(n, generator=g).to(DEV)
+    outs = {}
+    for out in (torch.float32, torch.bfloat16):
+        C = torch.empty(m, n, device=DEV, dtype=out)
+        with option("gemm_stream_out", stream):
+            ops.gemm([A], [B], [C], m=m, n=n, k=k, lda=k, ldb=k, ldc=n, a_kouter=False, b_kouter=False, dtype=dt,
+                     out_dtype=out, bias=[bias], alpha=0.75, drop_seed=77, drop_p=0.1, splits=1)
+        outs[out] = C
+    want = outs[torch.float32].to(torch.bfloat16)
+    bad = int((outs[torch.bfloat16].view(torch.int16) != want.view(torch.int16)).sum())
+    assert bad == 0, f"{bad} of {m * n} bf16 outputs differ from the rounded fp32 outputs"
+    ref = 0.75 * (A.float() @ B.float().t()) + bias
+    got = outs[torch.float32]
+    kept = got != 0
+    assert rel_err(got[kept] / (1 / 0.9), ref[kept]) < 1e-5
+    frac = 1 - float(kept.float().mean())
+    assert 0.08 < frac < 0.12, frac

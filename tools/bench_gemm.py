@@ -21,6 +21,10 @@ SHAPES = {  # name: (m, n, k, a_kouter, b_kouter, nbatch, out_bf16)
     "proj_l1_n768": (2097152, 768, 1024, 0, 0, 2, 1),
     "sq_k1024": (16384, 16384, 1024, 0, 0, 1, 1),
 }
+# K sweep at the input-projection M/N (persistent kernel up to 24 K-tiles): separates the
+# per-tile cost from the per-K-tile cost
+for _k in (128, 192, 320, 512, 768, 1024, 1536):
+    SHAPES[f"proj_k{_k}"] = (524288, 3072, _k, 0, 0, 2, 1)
 
 
 def run(name, iters, lda_pad=0):

@@ -259,22 +259,135 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_kernel(GemmArgs g) {
   }
 }
 
+// ---- direct epilogue of a 256x256 tile accumulated transposed (Loop8 CT) ----------
+// The wave's 128 x 64 block sits at (wm, wn) and acc[i][j][r] = C(wm + 16i + (lane & 15),
+// wn + 16j + 4 (lane >> 4) + r), so no LDS staging is needed: alpha / bias / relu /
+// dropout in fp32, then
+//   bf16: pack pairs and exchange column tiles j, j+1 with one v_permlane16_swap per
+//         dword: lane group q then holds columns 16 (j + (q & 1)) + 8 (q >> 1) .. +7 of its
+//         row, one 16-byte store per (i, j pair) -> 16 stores per wave;
+//   fp32: each lane's 4 columns are one 16-byte store -> 32 stores per wave.
+// A wave of a full tile (every row and column in range, vector-aligned C) issues exactly
+// EPI_STORES<TO> stores, which the persistent kernel's next counted wait allows for.
+template <typename TO>
+constexpr int EPI_STORES = sizeof(TO) == 2 ? 16 : 32;
+
+template <typename TO>
+TT_DEV void epi_direct(const GemmArgs& g, const f32x4 (&acc)[8][4], TO* C, const float* bias, int m0, int n0,
+                       int wm, int wn, bool full) {
+  const int lane = threadIdx.x & 63, q = lane >> 4, lr = lane & 15;
+  float bv[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bv[j][e] = 0.f;
+  if (bias) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = n0 + wn + 16 * j + 4 * q;
+      if (full && g.bias_vec_ok) {
+        const float4 b4 = *reinterpret_cast<const float4*>(bias + c);
+        bv[j][0] = b4.x; bv[j][1] = b4.y; bv[j][2] = b4.z; bv[j][3] = b4.w;
+      } else {
+        for (int e = 0; e < 4; ++e)
+          if (c + e < g.N) bv[j][e] = bias[c + e];
+      }
+    }
+  }
+#ifdef TT_DIAG
+  if (g.force_regstage == 9) {  // diagnostic build only: no stores (every accumulator stays live)
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sum += acc[i][j][0] + acc[i][j][3] + bv[j][0];
+    if (sum == 12345.f) C[0] = (TO)0;
+    return;
+  }
+#endif
+  const __amdgpu_buffer_rsrc_t crs = tt_rsrc(C + (long)m0 * g.ldc + n0);
+  auto fin = [&](float x, float b, int gm, int gn) {
+    x = x * g.alpha + b;
+    if (g.relu) x = fmaxf(x, 0.f);
+    if (g.drop_thresh) x *= tt_dropout_scale(g.drop_seed, g.drop_row0 + (uint32_t)gm, gn, g.drop_thresh, g.drop_inv_keep);
+    return x;
+  };
+  auto put = [&](int gm, int gn, uint4 v) {
+    if (g.stream_out) st16_sc1(crs, (int)(((long)(gm - m0) * g.ldc + (gn - n0)) * (long)sizeof(TO)), v);
+    else *reinterpret_cast<uint4*>(C + (long)gm * g.ldc + gn) = v;
+  };
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int gm = m0 + wm + 16 * i + lr;
+    if constexpr (sizeof(TO) == 2) {
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        uint32_t w[2][2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int j = 2 * jp + h, c = n0 + wn + 16 * j + 4 * q;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fin(acc[i][j][e], bv[j][e], gm, c + e);
+          w[h][0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          w[h][1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        }
+        const auto s0 = __builtin_amdgcn_permlane16_swap(w[0][0], w[1][0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(w[0][1], w[1][1], false, false);
+        const uint4 v = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        const int cs = n0 + wn + 16 * (2 * jp + (q & 1)) + 8 * (q >> 1);
+        if (full) {
+          put(gm, cs, v);
+        } else if (gm < g.M) {
+          if (cs + 8 <= g.N && g.vec_ok) {
+            put(gm, cs, v);
+          } else {
+            const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+            for (int e = 0; e < 8 && cs + e < g.N; ++e)
+              Elt<TO>::st(C + (long)gm * g.ldc + cs + e, __uint_as_float(e & 1 ? u[e >> 1] & 0xFFFF0000u : u[e >> 1] << 16));
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = n0 + wn + 16 * j + 4 * q;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fin(acc[i][j][e], bv[j][e], gm, c + e);
+        const uint4 u = make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                                   __float_as_uint(v[3]));
+        if (full) {
+          put(gm, c, u);
+        } else if (gm < g.M) {
+          if (c + 4 <= g.N && g.vec_ok) put(gm, c, u);
+          else
+            for (int e = 0; e < 4 && c + e < g.N; ++e) Elt<TO>::st(C + (long)gm * g.ldc + c + e, v[e]);
+        }
+      }
+    }
+  }
+}
+
 // ---- persistent 256x256 GEMM: one workgroup per CU walks tiles w, w+nwg, ... and the
 // 8-phase K-tile stream runs straight across tile boundaries: the last K-tiles of tile
 // i prefetch the first K-tiles of tile i+nwg (their pieces re-resolved on the fly), so
 // tile i's epilogue (32-row LDS passes, separate 32 KiB) runs while tile i+nwg's first
 // half-tiles land. No split-K, no accumulate-into-C (those use gemm_kernel).
-// A3: A prefetched two K-tiles ahead through a 3-slot ring (Loop8 A3 layout, 160 KiB);
-// the epilogue then stages in the A slot the tile's last K-tile has just consumed, which
-// the next tile's first K-tile refills only after the epilogue's last barrier.
+// A3 (default): A prefetched two K-tiles ahead through a 3-slot ring (Loop8 A3 layout,
+// 160 KiB), the product accumulated transposed and stored by epi_direct straight from
+// registers: no LDS and no barrier between tiles, so the K-tile stream never pauses; the
+// first counted wait of the next tile lets the epilogue's stores stay in flight. Measured
+// before this: the LDS-staged epilogue plus its barriers cost ~20k cycles per tile, more
+// than the 5 K-tiles of MFMAs of input_proj_l0.
 template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO, bool A3>
 __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
-  using L8 = ttg::Loop8<T, AKO, BKO, false, A3>;
+  using L8 = ttg::Loop8<T, AKO, BKO, false, A3, A3>;  // A3: transposed accumulate, direct epilogue
   using Piece = typename L8::Piece;
   constexpr int STG = A3 ? 0 : 32 * 256 * 4;
   static_assert(!A3 || 2 * L8::HALF >= 32 * 256 * 4, "staging fits an A slot");
   __shared__ __attribute__((aligned(16))) char lds[L8::LDS_BYTES + STG];
-  float* stg = reinterpret_cast<float*>(lds + L8::LDS_BYTES);  // !A3; A3: set per tile
+  float* stg = reinterpret_cast<float*>(lds + L8::LDS_BYTES);  // !A3 only
   const int nwg = gridDim.x;
   const int w = xcd_remap(blockIdx.x, nwg);
   if (w >= ntiles) return;
@@ -356,6 +469,7 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
   int git = 0;  // running K-tile index of the stream (slot parity)
   int as = 0;   // A3: A slot of the stream's current K-tile (git mod 3)
   int ra_off = 0, rb_off = 0;  // K-tile index of the A / B pieces' tile start in this tile's terms
+  bool epi_full = false;       // A3: the previous tile's epilogue issued EPI_STORES<TO> stores per wave
   for (int q = w; q < ntiles; q += nwg) {
     const int qn = q + nwg;
     const TileId cur_t = decode(q);
@@ -404,11 +518,25 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
         L8::issue_half(lb, pb0, r + 2 - rb_off, db, bcur);
         L8::quad(1, 1, fa, fb, acc);
         L8::issue_half(lb, pb1, r + 2 - rb_off, db, bcur + L8::HALF);
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        // K-tile r+1 landed; the 8 DMAs of r+2 stay in flight, and at r = 0 also the
+        // previous tile's epilogue stores (issued after r+1's DMAs, before r+2's)
+        if (r == 0 && epi_full) {
+          if constexpr (EPI_STORES<TO> == 16) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        }
         L8::quad(1, 0, fa, fb, acc);
-        if (r + 1 == nk) stg = reinterpret_cast<float*>(lds + as * (2 * L8::HALF));  // consumed: staging
         as = as == 2 ? 0 : as + 1;
       }
+      ra_off -= nk;
+      rb_off -= nk;
+      // epilogue straight from the accumulators: no LDS, no barrier, so the K-tile stream
+      // (and the two wave rows' one-barrier stagger) runs on into tile qn unchanged
+      const bool full = cur_t.m0 + 256 <= g.M && cur_t.n0 + 256 <= g.N && g.vec_ok;
+      epi_direct<TO>(g, acc, static_cast<TO*>(g.c[cur_t.bi]), g.bias[cur_t.bi], cur_t.m0, cur_t.n0, wm, wn, full);
+      epi_full = __builtin_amdgcn_readfirstlane((int)full) != 0;
+      continue;
     }
     for (int r = 0; r < (A3 ? 0 : nk); ++r, ++git) {
       const int cs = git & 1;
@@ -517,6 +645,8 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
     }
     if (late && qn < ntiles) __builtin_amdgcn_s_barrier();  // re-stagger for the next tile
   }
+  if constexpr (A3)
+    if (!late) __builtin_amdgcn_s_barrier();  // the late row's extra prologue barrier
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing zero-page DMAs land before exit
 }
 
@@ -597,7 +727,7 @@ int launch_gemm(int akout, int bkout, bool shift, GemmArgs& g, int nbatch, hipSt
   // slower at 48 and 128), no split-K, no accumulate (env TT_GEMM_PERSIST=0 disables)
   const bool persist_ok = tt::opt(tt::OPT_GEMM_PERSIST) != 0;
   const int nk = (g.K * (int)sizeof(T) + ttg::KTB - 1) / ttg::KTB;
-  if (dma && persist_ok && g.force_regstage == 0 && g.splits == 1 && !g.beta && nk >= 2 && nk <= TT_PERSIST_MAXK && t256 >= 512 &&
+  if (dma && persist_ok && (g.force_regstage == 0 || g.force_regstage == 9) && g.splits == 1 && !g.beta && nk >= 2 && nk <= TT_PERSIST_MAXK && t256 >= 512 &&
       use_big(g.M, g.N, t256))
     return launch_persist<T, TO>(akout, bkout, shift, g, (int)t256, st);
   if (dma && g.force_regstage != 2 && use_big(g.M, g.N, t256)) {

@@ -452,7 +452,10 @@ struct DLoop {
 // 0, 32, 64 KiB, B slots at 96, 128 KiB. A of K-tile r+2 goes into the slot K-tile r-1
 // used (both wave rows finished reading it one interval before this K-tile's P1); every
 // K-tile then has 8 DMAs per wave in flight at its wait (vmcnt(8)).
-template <typename T, bool AKO, bool BKO, bool BAL = false, bool A3 = false>
+// CT: accumulate the transposed product (B fragment as the MFMA's first operand), so that
+// acc[i][j][r] is C(16i + (lane & 15), 16j + 4 (lane >> 4) + r): every lane holds 4
+// consecutive output columns of one row, which an epilogue stores straight from registers.
+template <typename T, bool AKO, bool BKO, bool BAL = false, bool A3 = false, bool CT = false>
 struct Loop8 {
   static constexpr int HALF = 16384, SLOT = 4 * HALF, LDS_BYTES = A3 ? 10 * HALF : 2 * SLOT;
   static constexpr int BOFF = 6 * HALF;  // A3: first B slot
@@ -537,7 +540,8 @@ struct Loop8 {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[4 * mi + i][2 * ni + j] = mma<T>(fa[ks][i], fb[ks][2 * ni + j], acc[4 * mi + i][2 * ni + j]);
+          acc[4 * mi + i][2 * ni + j] = CT ? mma<T>(fb[ks][2 * ni + j], fa[ks][i], acc[4 * mi + i][2 * ni + j])
+                                           : mma<T>(fa[ks][i], fb[ks][2 * ni + j], acc[4 * mi + i][2 * ni + j]);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
   }

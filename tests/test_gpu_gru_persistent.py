@@ -154,3 +154,22 @@ def test_wave_owned_rows_forward_matches_per_step(H, B, T):
     with option("gru_fwd_wr", 1):
         outs_p = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=0)
     _assert_equivalent(outs_p, outs_s, B, T, H, bhn)
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+@pytest.mark.parametrize("H,B,T", [(512, 8192, 64), (512, 1000, 12), (256, 1000, 12), (512, 70, 3), (256, 64, 1)])
+def test_paired_ktile_forward_matches_per_step(H, B, T, mode):
+    """The persistent forward's alternative K-tile schedules (option gru_fwd_pair): 1 = two
+    K-tiles per barrier through a 4-stage W_hh ring whose extra stages are the gate staging
+    area (gru_fwd_seq<4, H/64, true>); 2 = one K-tile per barrier with both sub-steps'
+    fragments requested at once around the ring set's LDS store (early write); 3 / 4 = the
+    default schedule with the outputs deferred into the next block's K-tiles (4 and 2 W_hh
+    register sets). Same MFMA k
+    order and gate arithmetic as the per-step kernel, so every output is bit-identical -- at
+    the bench grid, with tail workgroups and at T = 1."""
+    ntow = 2
+    G, whh, bhn = _inputs(ntow, B, T, H, seed=7 * H + B + T)
+    outs_s = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=1)
+    with option("gru_fwd_pair", mode):
+        outs_p = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=0)
+    _assert_equivalent(outs_p, outs_s, B, T, H, bhn)

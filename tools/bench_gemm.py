@@ -20,6 +20,9 @@ SHAPES = {  # name: (m, n, k, a_kouter, b_kouter, nbatch, out_bf16)
     "input_proj_l0_k304": (524288, 3072, 304, 0, 0, 2, 1),
     "proj_l1_n768": (2097152, 768, 1024, 0, 0, 2, 1),
     "sq_k1024": (16384, 16384, 1024, 0, 0, 1, 1),
+    # configs[4] (H 1024, T 128, B 8192): input projection l1 and dX l1
+    "c4_proj_l1": (1048576, 6144, 2048, 0, 0, 2, 1),
+    "c4_dgrad_l1": (1048576, 2048, 6144, 0, 1, 1, 1),
 }
 # K sweep at the input-projection M/N (persistent kernel up to 24 K-tiles): separates the
 # per-tile cost from the per-K-tile cost

@@ -1,0 +1,8 @@
+set -o pipefail
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out
+mkdir -p $OUT
+cd $ROOT
+
+timeout -k 10 300 python tools/bench_gru.py --bwd-variants "" --iters 3 --variants seq:0,pair:0,seq:0,pair:0 > $OUT/gru_pair_o.log 2>&1 || exit 3
+echo done

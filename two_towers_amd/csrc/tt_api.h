@@ -32,6 +32,9 @@ enum Opt {
   OPT_GRU_FWD_RR,       // 1/2/3: experimental 128-row forward with gates in registers (bf16, H 512)
   OPT_GRU_FWD_WR,       // 1: wave-owned-rows persistent forward (bf16, H 256 / 512; h in registers)
   OPT_HN_MAP,           // hn_scan block -> (row tile, split) map: 0 split per XCD, 1 row tile per XCD
+  OPT_GEMM_SKEW,        // persistent GEMM: start workgroup w after (w % 4) * skew * 4096 cycles
+  OPT_GEMM_PERSIST_MAXK,  // persistent GEMM for problems of at most this many K-tiles
+  OPT_GRU_FWD_PAIR,     // persistent forward: two K-tiles per barrier (4-stage W_hh ring)
   OPT_N
 };
 int opt(Opt o);

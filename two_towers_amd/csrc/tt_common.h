@@ -100,6 +100,11 @@ TT_DEV uint4 ld16_buf(__amdgpu_buffer_rsrc_t r, uint32_t voff, int soff) {
   const tt_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, soff, AUX);
   return make_uint4(v[0], v[1], v[2], v[3]);
 }
+template <int AUX>
+TT_DEV void st16_buf_aux(__amdgpu_buffer_rsrc_t r, int off, uint4 v) {  // 2 nt, 17 sc0 sc1
+  tt_u32x4 w = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, AUX);
+}
 TT_DEV void st16_sc1(__amdgpu_buffer_rsrc_t r, int off, uint4 v) {
   tt_u32x4 w = {v.x, v.y, v.z, v.w};
   __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 16);

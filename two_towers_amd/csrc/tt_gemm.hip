@@ -36,6 +36,8 @@ constexpr OptDef kOpts[OPT_N] = {
     {"gru_bwd_phase", "TT_GRU_BWD_PHASE", 0},     {"gru_fwd_step_rows", "TT_GRU_FWD_STEP_ROWS", 0},
     {"infonce_flash", "TT_INFONCE_FLASH", 1},     {"gru_fwd_rr", "TT_GRU_FWD_RR", 0},
     {"gru_fwd_wr", "TT_GRU_FWD_WR", 0},           {"hn_map", "TT_HN_MAP", 0},
+    {"gemm_skew", "TT_GEMM_SKEW", 0},             {"gemm_persist_maxk", "TT_GEMM_PERSIST_MAXK", 24},
+    {"gru_fwd_pair", "TT_GRU_FWD_PAIR", 0},
 };
 struct OptTable {
   std::atomic<int> v[OPT_N];
@@ -94,6 +96,7 @@ struct GemmArgs {
   long part_stride;  // elements between split partials (fp32), 0 if no split
   int vec_ok;        // C rows 16-byte aligned: 8-column vector stores allowed
   int force_regstage;
+  int skew;  // persistent GEMM start skew (OPT_GEMM_SKEW)
   int bias_vec_ok;  // every bias pointer 16-byte aligned
   int stream_out;   // write-through (sc1) output stores: big outputs
 };
@@ -313,7 +316,16 @@ TT_DEV void epi_direct(const GemmArgs& g, const f32x4 (&acc)[8][4], TO* C, const
     return x;
   };
   auto put = [&](int gm, int gn, uint4 v) {
-    if (g.stream_out) st16_sc1(crs, (int)(((long)(gm - m0) * g.ldc + (gn - n0)) * (long)sizeof(TO)), v);
+#ifdef TT_DIAG
+    if (g.force_regstage == 10) {  // diagnostic: same stores into a 64-row (L2-resident) window
+      *reinterpret_cast<uint4*>(C + (long)(gm & 63) * g.ldc + gn) = v;
+      return;
+    }
+#endif
+    const int off = (int)(((long)(gm - m0) * g.ldc + (gn - n0)) * (long)sizeof(TO));
+    if (g.stream_out == 2) st16_buf_aux<2>(crs, off, v);
+    else if (g.stream_out == 3) st16_buf_aux<17>(crs, off, v);
+    else if (g.stream_out) st16_sc1(crs, off, v);
     else *reinterpret_cast<uint4*>(C + (long)gm * g.ldc + gn) = v;
   };
 #pragma unroll
@@ -391,6 +403,9 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
   const int nwg = gridDim.x;
   const int w = xcd_remap(blockIdx.x, nwg);
   if (w >= ntiles) return;
+  // optional start skew: workgroups in four phases, so the tiles' output bursts (all CUs
+  // finish a tile at about the same time otherwise) spread over the tile period
+  for (int i = 0; i < (w & 3) * g.skew; ++i) __builtin_amdgcn_s_sleep(64);
   const int ntn = (g.N + 255) / 256, ntm = (g.M + 255) / 256;
   const int nk = (g.K * (int)sizeof(T) + ttg::KTB - 1) / ttg::KTB;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, tid = threadIdx.x;
@@ -433,6 +448,23 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
       return ttg::KOPlain<T>{B, g.ldb, t.n0, q < ntiles ? g.N - t.n0 : 0};
     }
   };
+#ifdef TT_DIAG
+  if constexpr (A3) {
+    if (g.force_regstage == 11) {  // diagnostic build only: the epilogue stores alone, no K loop
+      f32x4 acc[8][4];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{(float)i, (float)j, 1.f, 2.f};
+      for (int q = w; q < ntiles; q += nwg) {
+        const TileId t = decode(q);
+        const bool full = t.m0 + 256 <= g.M && t.n0 + 256 <= g.N && g.vec_ok;
+        epi_direct<TO>(g, acc, static_cast<TO*>(g.c[t.bi]), g.bias[t.bi], t.m0, t.n0, wm, wn, full);
+      }
+      return;
+    }
+  }
+#endif
   auto la = loader_a(w);
   auto lb = loader_b(w);
   Piece pa0[2], pa1[2], pb0[2], pb1[2];
@@ -713,9 +745,6 @@ int launch_persist(int akout, int bkout, bool shift, const GemmArgs& g, int ntil
   return 0;
 }
 
-#ifndef TT_PERSIST_MAXK
-#define TT_PERSIST_MAXK 24
-#endif
 template <typename T, typename TO>
 int launch_gemm(int akout, int bkout, bool shift, GemmArgs& g, int nbatch, hipStream_t st) {
   constexpr int EPC = 16 / (int)sizeof(T);
@@ -727,7 +756,7 @@ int launch_gemm(int akout, int bkout, bool shift, GemmArgs& g, int nbatch, hipSt
   // slower at 48 and 128), no split-K, no accumulate (env TT_GEMM_PERSIST=0 disables)
   const bool persist_ok = tt::opt(tt::OPT_GEMM_PERSIST) != 0;
   const int nk = (g.K * (int)sizeof(T) + ttg::KTB - 1) / ttg::KTB;
-  if (dma && persist_ok && (g.force_regstage == 0 || g.force_regstage == 9) && g.splits == 1 && !g.beta && nk >= 2 && nk <= TT_PERSIST_MAXK && t256 >= 512 &&
+  if (dma && persist_ok && (g.force_regstage == 0 || g.force_regstage >= 9) && g.splits == 1 && !g.beta && nk >= 2 && nk <= tt::opt(tt::OPT_GEMM_PERSIST_MAXK) && t256 >= 512 &&
       use_big(g.M, g.N, t256))
     return launch_persist<T, TO>(akout, bkout, shift, g, (int)t256, st);
   if (dma && g.force_regstage != 2 && use_big(g.M, g.N, t256)) {
@@ -807,6 +836,7 @@ extern "C" int tt_gemm(int dtype, int out_dtype, int a_kouter, int b_kouter, int
   g.M = m; g.N = n; g.K = k;
   g.alpha = alpha; g.beta = beta_accum; g.relu = relu; g.seq_t = seq_t;
   g.force_regstage = tt::opt(tt::OPT_GEMM_REGSTAGE);
+  g.skew = tt::opt(tt::OPT_GEMM_SKEW);
   g.drop_seed = drop_seed;
   g.drop_row0 = batch->drop_row0;
   g.drop_thresh = drop_p > 0.f ? (uint32_t)(drop_p * 16777216.0f + 0.5f) : 0u;
@@ -827,7 +857,7 @@ extern "C" int tt_gemm(int dtype, int out_dtype, int a_kouter, int b_kouter, int
     // outputs far larger than the L2s are streamed past them (sc1); ld*rows must
     // stay addressable by a 32-bit per-tile byte offset
     g.stream_out = ok && (long)m * n * osz >= (64L << 20) && (long)256 * ldc * osz < (1L << 31);
-    g.stream_out = g.stream_out && tt::opt(tt::OPT_GEMM_STREAM_OUT) != 0;
+    g.stream_out = g.stream_out ? tt::opt(tt::OPT_GEMM_STREAM_OUT) : 0;  // 1 sc1, 2 nt, 3 sc0 sc1 (persistent)
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
   TT_CHECK_ARG((long)tt_ceil_div(m, 128) * tt_ceil_div(n, 128) * nbatch * splits < (1L << 31), "tt_gemm: too many tiles");

@@ -1105,9 +1105,41 @@ __device__ unsigned long long g_fwd_prof[2048][8];
 #define TT_PROF_PARAM
 #define TT_PROF_ARGS
 #endif
-template <int D>
+template <int D, bool EW = false>
 TT_DEV void fwd_kstep(const bf16_t* W, int H, int Q, int q, int kt, bool mm, const char* hb, char* bst, int& it,
                       int wm, int wn, f32x4 (&acc)[2][3], WTile& X, WTile& Y TT_PROF_PARAM) {
+  if constexpr (EW) {
+    // early-write order: both sub-steps' fragments requested at once with the ring set's
+    // LDS store between them, so the second read latency and the store transfer run under
+    // the first sub-step's MFMAs instead of after the last one
+    fwd_load_b(W, H, (q + D) % Q, Y);
+    const char* ia = hb + kt * (PR * ttg::KTB);
+    const char* ib = bst + (it & 1) * P_BST;
+    uint4 fa[2][2], fb[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) fa[0][i] = ttg::frag<bf16_t, false>(ia, wm + 16 * i, 0);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) fb[0][j] = ttg::frag<bf16_t, false>(ib, wn + 16 * j, 0);
+    fwd_store_b(bst + ((it + 1) & 1) * P_BST, X);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) fa[1][i] = ttg::frag<bf16_t, false>(ia, wm + 16 * i, 1);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) fb[1][j] = ttg::frag<bf16_t, false>(ib, wn + 16 * j, 1);
+    if (mm) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) acc[i][j] = ttg::mma<bf16_t>(fb[ks][j], fa[ks][i], acc[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    __syncthreads();
+    ++it;
+    return;
+  }
   TT_STAMP(t0);
 #ifdef TT_DIAG
   if (!(dbg & 16)) fwd_load_b(W, H, (q + D) % Q, Y);  // 16: no W_hh loads
@@ -1145,13 +1177,56 @@ TT_DEV void fwd_kstep(const bf16_t* W, int H, int Q, int q, int kt, bool mm, con
   ++it;
 }
 
+// P2 form: two K-tiles per barrier through a 4-stage W_hh ring (the two extra stages are
+// the gate staging area, free during the K loop): read K-tiles it, it+1 from stages
+// it % 4, (it+1) % 4, store the register pair X (K-tiles it+2, it+3, loaded one interval
+// ago) into the two other stages, load it+4, it+5 into the pair Y. The stages written
+// here were last read in the previous interval, before its barrier.
+TT_DEV char* fwd_stage(char* lds, int i) { return lds + P_HB + (i & 3) * P_BST; }
+TT_DEV void fwd_kpair(const bf16_t* W, int H, int Q, int q, int kt, bool mm, const char* hb, char* lds, int& it,
+                      int wm, int wn, f32x4 (&acc)[2][3], WTile& X0, WTile& X1, WTile& Y0, WTile& Y1) {
+  fwd_load_b(W, H, (q + 4) % Q, Y0);
+  fwd_load_b(W, H, (q + 5) % Q, Y1);
+  if (mm) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const char* ia = hb + (kt + h) * (PR * ttg::KTB);
+      const char* ib = fwd_stage(lds, it + h);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        uint4 fa[2], fb[3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) fa[i] = ttg::frag<bf16_t, false>(ia, wm + 16 * i, ks);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) fb[j] = ttg::frag<bf16_t, false>(ib, wn + 16 * j, ks);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) acc[i][j] = ttg::mma<bf16_t>(fb[j], fa[i], acc[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  }
+  fwd_store_b(fwd_stage(lds, it + 2), X0);
+  fwd_store_b(fwd_stage(lds, it + 3), X1);
+  __syncthreads();
+  it += 2;
+}
+
 // Whh K-tiles in flight in registers: 1, 2 or 4 (D divides H/64); NKT = H/64 when known
 // at compile time (0: runtime). A compile-time NKT unrolls the block's K loop, so hipcc's
 // vmcnt bookkeeping at its first K-tiles counts the previous block's epilogue stores and
 // the gate loads exactly instead of the loop-merged minimum: with one in-order counter
 // that minimum made the first W_hh waits of every block also wait for those stores.
-template <int D, int NKT>
+// DS (deferred stores): a block's six 16-byte outputs per thread stay packed in registers
+// and are issued one per K-tile during the next block's first six K-tiles (the last
+// block's after the step loop), so the HBM writes run under the W_hh stream and the MFMAs
+// instead of in a burst at every block's end; the first block's six slots are dropped
+// stores (out-of-range offset), so every K-tile issues the same count.
+template <int D, int NKT, bool P2 = false, bool EW = false, bool DS = false, bool TM = false>
 __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
+  static_assert(!P2 || (D == 4 && NKT % 4 == 0 && NKT > 0), "paired K-tiles: 4 register sets, NKT % 4 == 0");
   __shared__ __attribute__((aligned(16))) char lds[P_LDS];
   char* hb = lds;
   char* bst = lds + P_HB;
@@ -1178,11 +1253,12 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
   // row: no branches around the memory instructions (a tail row's offset is out of
   // range, so it reads zeros and its stores are dropped; no X1 = num_records 0), so
   // every wave issues the same count and the waits above stay exact
+  // TM (time-major rows t*B + b, timing experiment): the resources are rebased every step
   const long r0w = (long)m0 * T_;
-  const __amdgpu_buffer_rsrc_t rG = tt_rsrc_n(G + r0w * a.ldg, true);
-  const __amdgpu_buffer_rsrc_t rY = tt_rsrc_n(Yw + r0w * a.ldy, true);
-  const __amdgpu_buffer_rsrc_t rX1 = tt_rsrc_n(X1 ? X1 + r0w * a.ldy : Yw, X1 != nullptr);
-  const __amdgpu_buffer_rsrc_t rS = tt_rsrc_n(S + r0w * 4L * H, true);
+  __amdgpu_buffer_rsrc_t rG = tt_rsrc_n(G + r0w * a.ldg, true);
+  __amdgpu_buffer_rsrc_t rY = tt_rsrc_n(Yw + r0w * a.ldy, true);
+  __amdgpu_buffer_rsrc_t rX1 = tt_rsrc_n(X1 ? X1 + r0w * a.ldy : Yw, X1 != nullptr);
+  __amdgpu_buffer_rsrc_t rS = tt_rsrc_n(S + r0w * 4L * H, true);
 #ifdef TT_DIAG
   const bool gok = rowok && !(a.dbg & 2), sok = rowok && !(a.dbg & 1);
 #else
@@ -1201,12 +1277,21 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
     for (int e = 0; e < 8; ++e) hreg[i][e] = 0.f;
 
   WTile r0, r1, r2, r3;
-  fwd_load_b(W, H, qoff, r0);
-  fwd_store_b(bst, r0);
-  if (D >= 2) fwd_load_b(W, H, (qoff + 1) % Q, r1);
-  if (D >= 4) {
-    fwd_load_b(W, H, (qoff + 2) % Q, r2);
-    fwd_load_b(W, H, (qoff + 3) % Q, r3);
+  if constexpr (P2) {  // K-tiles 0, 1 into stages 0, 1; 2, 3 in the register pair (r0, r1)
+    fwd_load_b(W, H, qoff, r0);
+    fwd_load_b(W, H, (qoff + 1) % Q, r1);
+    fwd_store_b(fwd_stage(lds, 0), r0);
+    fwd_store_b(fwd_stage(lds, 1), r1);
+    fwd_load_b(W, H, (qoff + 2) % Q, r0);
+    fwd_load_b(W, H, (qoff + 3) % Q, r1);
+  } else {
+    fwd_load_b(W, H, qoff, r0);
+    fwd_store_b(bst, r0);
+    if (D >= 2) fwd_load_b(W, H, (qoff + 1) % Q, r1);
+    if (D >= 4) {
+      fwd_load_b(W, H, (qoff + 2) % Q, r2);
+      fwd_load_b(W, H, (qoff + 3) % Q, r3);
+    }
   }
   int it = 0;  // running K-tile counter: Whh stage = it & 1
 #ifdef TT_DIAG
@@ -1217,13 +1302,32 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
   // six dropped stores (out-of-range offset) stand in for the epilogue's six, so every
   // path into a block's first K-tiles has the same pending count and hipcc's waits
   // there leave the stores in flight
+  uint4 pend[6];  // DS: the previous block's packed outputs: Y, S r / z / n / gh_n, X1
+  uint32_t poy = 0x80000000u, pos = 0x80000000u;
+  if constexpr (DS) {
 #pragma unroll
-  for (int q = 0; q < 6; ++q) st16_buf(rY, 0x80000000u + 16u * q, 0, make_uint4(0, 0, 0, 0));
+    for (int q = 0; q < 6; ++q) pend[q] = make_uint4(0, 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 6; ++q) st16_buf(rY, 0x80000000u + 16u * q, 0, make_uint4(0, 0, 0, 0));
+  }
+  auto flush = [&](int q) {  // DS: issue pending output q (q compile-time after unrolling)
+    if (q == 0) st16_buf(rY, poy, 0, pend[0]);
+    else if (q < 5) st16_buf(rS, pos, (q - 1) * 2 * H, pend[q]);
+    else st16_buf(rX1, poy, 0, pend[5]);
+  };
 
   for (int s = 0; s < T_; ++s) {
     const int t = R.dir ? T_ - 1 - s : s;
     const long row = (long)b * T_ + t;
-    const int lrow = rl * T_ + t;  // row within this workgroup's resources
+    const int lrow = TM ? rl : rl * T_ + t;  // row within this workgroup's resources
+    if constexpr (TM) {
+      const long tr = (long)t * a.B + m0;
+      rG = tt_rsrc_n(G + tr * a.ldg, true);
+      rY = tt_rsrc_n(Yw + tr * a.ldy, true);
+      rX1 = tt_rsrc_n(X1 ? X1 + tr * a.ldy : Yw, X1 != nullptr);
+      rS = tt_rsrc_n(S + tr * 4L * H, true);
+    }
 #pragma unroll 1
     for (int blk0 = 0; blk0 < nblk; ++blk0) {
       const int blk = blk0 + boff < nblk ? blk0 + boff : blk0 + boff - nblk;
@@ -1243,18 +1347,42 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
 #pragma unroll
           for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         // ring of D register sets: iteration q reads set (q+1)%D, refills set q%D
-#define TT_KS(j, X, Y) fwd_kstep<D>(W, H, Q, blk * nkt + kt + j, kt + j, s > 0, hb, bst, it, wm, wn, acc, X, Y TT_PROF_ARGS)
-        if constexpr (D == 1) {
+#define TT_KS(j, X, Y) fwd_kstep<D, EW>(W, H, Q, blk * nkt + kt + j, kt + j, s > 0, hb, bst, it, wm, wn, acc, X, Y TT_PROF_ARGS)
+        if constexpr (P2) {
+#pragma unroll
+          for (int kt = 0; kt < nkt; kt += 4) {
+            fwd_kpair(W, H, Q, blk * nkt + kt, kt, s > 0, hb, lds, it, wm, wn, acc, r0, r1, r2, r3);
+            fwd_kpair(W, H, Q, blk * nkt + kt + 2, kt + 2, s > 0, hb, lds, it, wm, wn, acc, r2, r3, r0, r1);
+          }
+        } else if constexpr (D == 1) {
 #pragma unroll
           for (int kt = 0; kt < nkt; ++kt) TT_KS(0, r0, r0);
         } else if constexpr (D == 2) {
 #pragma unroll
-          for (int kt = 0; kt < nkt; kt += 2) { TT_KS(0, r1, r0); TT_KS(1, r0, r1); }
+          for (int kt = 0; kt < nkt; kt += 2) {
+            TT_KS(0, r1, r0);
+            if constexpr (DS) { if (kt < 6) flush(kt); }
+            TT_KS(1, r0, r1);
+            if constexpr (DS) { if (kt + 1 < 6) flush(kt + 1); }
+          }
         } else {
 #pragma unroll
-          for (int kt = 0; kt < nkt; kt += 4) { TT_KS(0, r1, r0); TT_KS(1, r2, r1); TT_KS(2, r3, r2); TT_KS(3, r0, r3); }
+          for (int kt = 0; kt < nkt; kt += 4) {
+            TT_KS(0, r1, r0);
+            if constexpr (DS) { if (kt < 6) flush(kt); }
+            TT_KS(1, r2, r1);
+            if constexpr (DS) { if (kt + 1 < 6) flush(kt + 1); }
+            TT_KS(2, r3, r2);
+            if constexpr (DS) { if (kt + 2 < 6) flush(kt + 2); }
+            TT_KS(3, r0, r3);
+            if constexpr (DS) { if (kt + 3 < 6) flush(kt + 3); }
+          }
         }
 #undef TT_KS
+        if constexpr (DS) {  // fewer than six K-tiles per block: the rest of the previous block's outputs
+#pragma unroll
+          for (int q = NKT; q < 6; ++q) flush(q);
+        }
         TT_STAMP(e0);
         // gates -> LDS (fp32), then per-thread rows
         // (C^T accumulators: one 16-byte store per block instead of four 4-byte ones; ≈ 0.4 %,
@@ -1284,6 +1412,7 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
           lz[4 * h] = v1.x; lz[4 * h + 1] = v1.y; lz[4 * h + 2] = v1.z; lz[4 * h + 3] = v1.w;
           ln[4 * h] = v2.x; ln[4 * h + 1] = v2.y; ln[4 * h + 2] = v2.z; ln[4 * h + 3] = v2.w;
         }
+        if constexpr (P2) __syncthreads();  // stg = ring stages 2, 3: read before the next block restages them
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
 #ifdef TT_DIAG
@@ -1304,11 +1433,21 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
         {
           const uint32_t oy = sok ? (uint32_t)(lrow * (int)a.ldy + j) * 2u : 0x80000000u;
           const uint32_t os = sok ? (uint32_t)(lrow * 4 * H + j) * 2u : 0x80000000u;
-          st16_buf(rY, oy, 0, pack8bf(y));
-          st16_buf(rS, os, 0, pack8bf(sr));
-          st16_buf(rS, os, 2 * H, pack8bf(sz));
-          st16_buf(rS, os, 4 * H, pack8bf(sn));
-          st16_buf(rS, os, 6 * H, pack8bf(sg));
+          if constexpr (DS) {
+            pend[0] = pack8bf(y);
+            pend[1] = pack8bf(sr);
+            pend[2] = pack8bf(sz);
+            pend[3] = pack8bf(sn);
+            pend[4] = pack8bf(sg);
+            poy = oy;
+            pos = os;
+          } else {
+            st16_buf(rY, oy, 0, pack8bf(y));
+            st16_buf(rS, os, 0, pack8bf(sr));
+            st16_buf(rS, os, 2 * H, pack8bf(sz));
+            st16_buf(rS, os, 4 * H, pack8bf(sn));
+            st16_buf(rS, os, 6 * H, pack8bf(sg));
+          }
 #ifdef TT_DIAG
           if (X1 && a.drop_thresh && !(a.dbg & 32)) {  // 32: X1 copy without the mask hash
 #else
@@ -1319,7 +1458,8 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
               y[e] *= tt_dropout_scale(R.seed, R.row0 + (uint32_t)row, (uint32_t)(R.col0 + j + e), a.drop_thresh,
                                        a.inv_keep);
           }
-          st16_buf(rX1, oy, 0, pack8bf(y));
+          if constexpr (DS) pend[5] = pack8bf(y);
+          else st16_buf(rX1, oy, 0, pack8bf(y));
         }
         TT_STAMP(e2);
         TT_ACC(4, e2 - e1);  // gate math + stores issued
@@ -1357,6 +1497,10 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
       }
     }
     __syncthreads();
+  }
+  if constexpr (DS) {
+#pragma unroll
+    for (int q = 0; q < 6; ++q) flush(q);  // the last block's outputs
   }
 #ifdef TT_DIAG
   TT_STAMP(k_end);
@@ -2039,7 +2183,23 @@ extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B
     const dim3 grid(tt_ceil_div(B, PR) * nrec);
     int depth = (H / 64) % 4 == 0 ? 4 : (H / 64) % 2 == 0 ? 2 : 1;
     depth = std::min(depth, tt::opt(tt::OPT_GRU_DEPTH));
-    if (depth >= 4 && H == 512) hipLaunchKernelGGL((gru_fwd_seq<4, 8>), grid, dim3(PNT), 0, st, a);
+    const bool pair = depth >= 4 && tt::opt(tt::OPT_GRU_FWD_PAIR) == 1;
+    const bool ew = depth >= 4 && tt::opt(tt::OPT_GRU_FWD_PAIR) == 2;  // early-write K-tile order
+    const int fo = tt::opt(tt::OPT_GRU_FWD_PAIR);
+    if (fo == 5 && depth >= 4 && H == 512) {  // timing experiment only: time-major row addressing
+      hipLaunchKernelGGL((gru_fwd_seq<4, 8, false, false, false, true>), grid, dim3(PNT), 0, st, a);
+      TT_CHECK_LAUNCH("gru_fwd_seq");
+      return 0;
+    }
+    if (fo == 3 && depth >= 4 && H == 512) hipLaunchKernelGGL((gru_fwd_seq<4, 8, false, false, true>), grid, dim3(PNT), 0, st, a);
+    else if (fo == 3 && depth >= 4 && H == 256) hipLaunchKernelGGL((gru_fwd_seq<4, 4, false, false, true>), grid, dim3(PNT), 0, st, a);
+    else if (fo == 4 && depth >= 2 && H == 512) hipLaunchKernelGGL((gru_fwd_seq<2, 8, false, false, true>), grid, dim3(PNT), 0, st, a);
+    else if (fo == 4 && depth >= 2 && H == 256) hipLaunchKernelGGL((gru_fwd_seq<2, 4, false, false, true>), grid, dim3(PNT), 0, st, a);
+    else if (ew && H == 512) hipLaunchKernelGGL((gru_fwd_seq<4, 8, false, true>), grid, dim3(PNT), 0, st, a);
+    else if (ew && H == 256) hipLaunchKernelGGL((gru_fwd_seq<4, 4, false, true>), grid, dim3(PNT), 0, st, a);
+    else if (pair && H == 512) hipLaunchKernelGGL((gru_fwd_seq<4, 8, true>), grid, dim3(PNT), 0, st, a);
+    else if (pair && H == 256) hipLaunchKernelGGL((gru_fwd_seq<4, 4, true>), grid, dim3(PNT), 0, st, a);
+    else if (depth >= 4 && H == 512) hipLaunchKernelGGL((gru_fwd_seq<4, 8>), grid, dim3(PNT), 0, st, a);
     else if (depth >= 4 && H == 256) hipLaunchKernelGGL((gru_fwd_seq<4, 4>), grid, dim3(PNT), 0, st, a);
     else if (depth >= 4) hipLaunchKernelGGL((gru_fwd_seq<4, 0>), grid, dim3(PNT), 0, st, a);
     else if (depth == 2 && H == 512) hipLaunchKernelGGL((gru_fwd_seq<2, 8>), grid, dim3(PNT), 0, st, a);

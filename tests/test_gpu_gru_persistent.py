@@ -156,7 +156,7 @@ def test_wave_owned_rows_forward_matches_per_step(H, B, T):
     _assert_equivalent(outs_p, outs_s, B, T, H, bhn)
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4, 6])
 @pytest.mark.parametrize("H,B,T", [(512, 8192, 64), (512, 1000, 12), (256, 1000, 12), (512, 70, 3), (256, 64, 1)])
 def test_paired_ktile_forward_matches_per_step(H, B, T, mode):
     """The persistent forward's alternative K-tile schedules (option gru_fwd_pair): 1 = two
@@ -164,7 +164,7 @@ def test_paired_ktile_forward_matches_per_step(H, B, T, mode):
     area (gru_fwd_seq<4, H/64, true>); 2 = one K-tile per barrier with both sub-steps'
     fragments requested at once around the ring set's LDS store (early write); 3 / 4 = the
     default schedule with the outputs deferred into the next block's K-tiles (4 and 2 W_hh
-    register sets). Same MFMA k
+    register sets); 6 = gru_fwd_seq16 (16 waves, four per SIMD, 4 units per thread). Same MFMA k
     order and gate arithmetic as the per-step kernel, so every output is bit-identical -- at
     the bench grid, with tail workgroups and at T = 1."""
     ntow = 2

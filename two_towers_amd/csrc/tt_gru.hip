@@ -1800,6 +1800,179 @@ __global__ __launch_bounds__(NT) void gru_fwd_rr(FwdArgs a) {
 }
 
 
+// ---- persistent forward with 16 waves (four per SIMD), bf16, H 256 / 512 --------------
+// gru_fwd_seq's row-resident scheme -- 64 rows of one recurrence per workgroup, h_{s-1} as
+// the bf16 A image in LDS, W_hh streamed every step through a 2-stage LDS ring, the gates
+// staged once through LDS -- with twice the waves: 1024 threads as 4 (rows) x 4 (gate
+// columns), wave tile 16 x 48, every thread owning 4 units of one row (8-byte gate loads
+// and output stores: 16 lanes write a row's whole 128-byte line). At <= 128 VGPRs a SIMD
+// holds four waves instead of two, so one wave's fragment-read, W_hh-load and store
+// latencies overlap the other waves' MFMAs and gate arithmetic; the price is that every
+// B fragment is read by four waves (LDS reads per K-tile 128 KiB instead of 80). Same
+// MFMA k order and gate arithmetic as the per-step kernel: bit-identical outputs.
+namespace s16 {
+constexpr int NT = 1024;
+}
+struct S16Set {  // one thread's share of a W_hh K-tile (threads < 512 store both chunks)
+  uint4 v0, v1;
+};
+TT_DEV uint4 s16_chunk(const bf16_t* W, int H, int blk, int kt, int id) {
+  const int c = id & 7, row = id >> 3, g = row >> 6, u = row & 63;
+  return *reinterpret_cast<const uint4*>(W + (long)(g * H + blk * 64 + u) * H + kt * 64 + c * 8);
+}
+TT_DEV void s16_load_b(const bf16_t* W, int H, int q, int nkt, S16Set& r) {
+  const int blk = q / nkt, kt = q - blk * nkt;
+  const int t = threadIdx.x;
+  r.v0 = s16_chunk(W, H, blk, kt, t);
+  // 1536 16-byte chunks per K-tile: the second load of threads >= 512 repeats their first
+  // chunk (unconditional, so the set stays in registers) and is not stored
+  r.v1 = s16_chunk(W, H, blk, kt, t < 512 ? t + s16::NT : t);
+}
+TT_DEV void s16_store_b(char* img, const S16Set& r) {
+  const int t = threadIdx.x;
+  *reinterpret_cast<uint4*>(img + ttg::kc_off(t >> 3, t & 7)) = r.v0;
+  if (t < 512) *reinterpret_cast<uint4*>(img + ttg::kc_off((t + s16::NT) >> 3, t & 7)) = r.v1;
+}
+TT_DEV void st8_bufv(__amdgpu_buffer_rsrc_t r, uint32_t voff, int soff, uint2 v) {  // soff folded
+  typedef unsigned u32x2 __attribute__((vector_size(8)));
+  u32x2 w = {v.x, v.y};
+  __builtin_amdgcn_raw_buffer_store_b64(w, r, (int)(voff + (uint32_t)soff), 0, 0);
+}
+// one K-tile: refill register set Y with K-tile q+2, MFMAs on stage it&1, set X (K-tile
+// q+1) into the other stage, barrier
+TT_DEV void s16_kstep(const bf16_t* W, int H, int Q, int nkt, int q, int kt, bool mm, const char* hb, char* bst,
+                      int& it, int wm, int wn, f32x4 (&acc)[3], S16Set& X, S16Set& Y) {
+  s16_load_b(W, H, (q + 2) % Q, nkt, Y);
+  if (mm) {
+    const char* ia = hb + kt * (PR * ttg::KTB);
+    const char* ib = bst + (it & 1) * P_BST;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const uint4 fa = ttg::frag<bf16_t, false>(ia, wm, ks);
+      uint4 fb[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) fb[j] = ttg::frag<bf16_t, false>(ib, wn + 16 * j, ks);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc[j] = ttg::mma<bf16_t>(fb[j], fa, acc[j]);  // C^T, as gru_fwd_seq
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  s16_store_b(bst + ((it + 1) & 1) * P_BST, X);
+  __syncthreads();
+  ++it;
+}
+
+template <int NKT>
+__global__ __launch_bounds__(1024) void gru_fwd_seq16(FwdArgs a) {
+  static_assert(NKT == 4 || NKT == 8, "H 256 / 512");
+  __shared__ __attribute__((aligned(16))) char lds[P_LDS];
+  char* hb = lds;
+  char* bst = lds + P_HB;
+  float* stg = reinterpret_cast<float*>(lds + P_HB + 2 * P_BST);
+  const int ntm = (a.B + PR - 1) / PR;
+  const int id = ttg::xcd_remap(blockIdx.x, gridDim.x);
+  const int rz = id / ntm;
+  const FwdRec R = a.r[rz];
+  const int H = a.H, T_ = a.T;
+  const int m0 = (id - rz * ntm) * PR;
+  constexpr int nkt = NKT, Q = NKT * NKT;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = (wave >> 2) * 16, wn = (wave & 3) * 48;
+  const bf16_t* W = static_cast<const bf16_t*>(R.whh);
+  const bf16_t* G = static_cast<const bf16_t*>(R.g);
+  bf16_t* Yw = static_cast<bf16_t*>(R.y);
+  bf16_t* X1 = static_cast<bf16_t*>(R.x1);
+  bf16_t* S = static_cast<bf16_t*>(R.save);
+  const int rl = tid >> 4, jg = (tid & 15) * 4;  // epilogue: row rl, units blk*64 + jg .. +4
+  const int b = m0 + rl;
+  const bool rowok = b < a.B;
+  const long r0w = (long)m0 * T_;
+  const __amdgpu_buffer_rsrc_t rG = tt_rsrc_n(G + r0w * a.ldg, true);
+  const __amdgpu_buffer_rsrc_t rY = tt_rsrc_n(Yw + r0w * a.ldy, true);
+  const __amdgpu_buffer_rsrc_t rX1 = tt_rsrc_n(X1 ? X1 + r0w * a.ldy : Yw, X1 != nullptr);
+  const __amdgpu_buffer_rsrc_t rS = tt_rsrc_n(S + r0w * 4L * H, true);
+
+  float hreg[NKT][4];  // fp32 state of this thread's units; hreg[0] = the block being updated
+#pragma unroll
+  for (int i = 0; i < NKT; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) hreg[i][e] = 0.f;
+  S16Set r0, r1;
+  s16_load_b(W, H, 0, nkt, r0);
+  s16_store_b(bst, r0);
+  s16_load_b(W, H, 1, nkt, r1);
+  int it = 0;
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 6; ++q) st8_bufv(rY, 0x80000000u + 8u * q, 0, make_uint2(0, 0));  // as gru_fwd_seq
+
+  for (int s = 0; s < T_; ++s) {
+    const int t = R.dir ? T_ - 1 - s : s;
+    const long row = (long)b * T_ + t;
+    const int lrow = rl * T_ + t;
+#pragma unroll 1
+    for (int blk = 0; blk < NKT; ++blk) {
+      uint2 gx[3];
+      const uint32_t og = rowok ? (uint32_t)(lrow * (int)a.ldg + blk * 64 + jg) * 2u : 0x80000000u;
+#pragma unroll
+      for (int g = 0; g < 3; ++g) gx[g] = ld8_buf(rG, og, g * H * 2);
+      const float4 bn4 = *reinterpret_cast<const float4*>(R.bhn + blk * 64 + jg);
+      f32x4 acc[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kt = 0; kt < nkt; kt += 2) {
+        s16_kstep(W, H, Q, nkt, blk * nkt + kt, kt, s > 0, hb, bst, it, wm, wn, acc, r1, r0);
+        s16_kstep(W, H, Q, nkt, blk * nkt + kt + 1, kt + 1, s > 0, hb, bst, it, wm, wn, acc, r0, r1);
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        *reinterpret_cast<f32x4*>(stg + stg_off(wm + (lane & 15), wn + 16 * j + 4 * (lane >> 4))) = acc[j];
+      __syncthreads();
+      const float4 v0 = *reinterpret_cast<const float4*>(stg + stg_off(rl, 0 * 64 + jg));
+      const float4 v1 = *reinterpret_cast<const float4*>(stg + stg_off(rl, 1 * 64 + jg));
+      const float4 v2 = *reinterpret_cast<const float4*>(stg + stg_off(rl, 2 * 64 + jg));
+      const float lr[4] = {v0.x, v0.y, v0.z, v0.w}, lz[4] = {v1.x, v1.y, v1.z, v1.w}, ln[4] = {v2.x, v2.y, v2.z, v2.w};
+      const float bn[4] = {bn4.x, bn4.y, bn4.z, bn4.w};
+      float xr[4], xz[4], xn[4], y[4], sr[4], sz[4], sn[4], sg[4];
+      unpack4(gx[0], xr);
+      unpack4(gx[1], xz);
+      unpack4(gx[2], xn);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        gru_cell(xr[e], xz[e], xn[e], lr[e], lz[e], ln[e], bn[e], hreg[0][e], y[e], sr[e], sz[e], sn[e], sg[e]);
+      const int j = blk * 64 + jg;
+      const uint32_t oy = rowok ? (uint32_t)(lrow * (int)a.ldy + j) * 2u : 0x80000000u;
+      const uint32_t os = rowok ? (uint32_t)(lrow * 4 * H + j) * 2u : 0x80000000u;
+      st8_bufv(rY, oy, 0, pack4bf(y));
+      st8_bufv(rS, os, 0, pack4bf(sr));
+      st8_bufv(rS, os, 2 * H, pack4bf(sz));
+      st8_bufv(rS, os, 4 * H, pack4bf(sn));
+      st8_bufv(rS, os, 6 * H, pack4bf(sg));
+      float yd[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        yd[e] = (X1 && a.drop_thresh) ? y[e] * tt_dropout_scale(R.seed, R.row0 + (uint32_t)row, (uint32_t)(R.col0 + j + e),
+                                                                 a.drop_thresh, a.inv_keep)
+                                      : y[e];
+      st8_bufv(rX1, oy, 0, pack4bf(yd));
+#pragma unroll
+      for (int i = 0; i < NKT - 1; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) hreg[i][e] = hreg[i + 1][e];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) hreg[NKT - 1][e] = y[e];
+    }
+    // h_s -> A operand of step s+1 (every wave finished reading h_{s-1}: the last K-tile
+    // ended with a barrier); units jg .. +4 are half (jg & 4) of chunk jg >> 3
+#pragma unroll
+    for (int i = 0; i < NKT; ++i)
+      *reinterpret_cast<uint2*>(hb + i * (PR * ttg::KTB) + ttg::kc_off(rl, jg >> 3) + (jg & 4) * 2) = pack4bf(hreg[i]);
+    __syncthreads();
+  }
+}
+
 // ---- wave-owned-rows persistent forward (gru_fwd_wr, bf16, H 256 / 512) ------------------
 // Each of the 4 waves (one per SIMD) owns 16 batch rows of one recurrence for all T steps
 // and keeps, in its own registers, h_{s-1} as the MFMA operand (bf16, k-step kk = units
@@ -2186,6 +2359,12 @@ extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B
     const bool pair = depth >= 4 && tt::opt(tt::OPT_GRU_FWD_PAIR) == 1;
     const bool ew = depth >= 4 && tt::opt(tt::OPT_GRU_FWD_PAIR) == 2;  // early-write K-tile order
     const int fo = tt::opt(tt::OPT_GRU_FWD_PAIR);
+    if (fo == 6 && (H == 512 || H == 256)) {  // 16 waves per workgroup
+      if (H == 512) hipLaunchKernelGGL(gru_fwd_seq16<8>, grid, dim3(s16::NT), 0, st, a);
+      else hipLaunchKernelGGL(gru_fwd_seq16<4>, grid, dim3(s16::NT), 0, st, a);
+      TT_CHECK_LAUNCH("gru_fwd_seq16");
+      return 0;
+    }
     if (fo == 5 && depth >= 4 && H == 512) {  // timing experiment only: time-major row addressing
       hipLaunchKernelGGL((gru_fwd_seq<4, 8, false, false, false, true>), grid, dim3(PNT), 0, st, a);
       TT_CHECK_LAUNCH("gru_fwd_seq");

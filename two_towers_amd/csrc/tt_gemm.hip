@@ -552,7 +552,12 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
         L8::issue_half(lb, pb1, r + 2 - rb_off, db, bcur + L8::HALF);
         // K-tile r+1 landed; the 8 DMAs of r+2 stay in flight, and at r = 0 also the
         // previous tile's epilogue stores (issued after r+1's DMAs, before r+2's)
-        if (r == 0 && epi_full) {
+#ifdef TT_DIAG
+        const bool loose = g.force_regstage == 12 && r < 3 && epi_full;  // timing only: stores never waited for
+#else
+        constexpr bool loose = false;
+#endif
+        if ((r == 0 && epi_full) || loose) {
           if constexpr (EPI_STORES<TO> == 16) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
           else asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
         } else {

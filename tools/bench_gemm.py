@@ -30,6 +30,9 @@ for _k in (128, 192, 320, 512, 768, 1024, 1536):
     SHAPES[f"proj_k{_k}"] = (524288, 3072, _k, 0, 0, 2, 1)
 
 
+NO_BIAS = False
+
+
 def run(name, iters, lda_pad=0):
     m, n, k, ak, bk, nb, obf = SHAPES[name]
     dt = torch.bfloat16
@@ -42,7 +45,7 @@ def run(name, iters, lda_pad=0):
     B = [torch.randn((k, n) if bk else (n, k), device="cuda").to(dt) for _ in range(nb)]
     odt = dt if obf else torch.float32
     C = [torch.empty(m, n, device="cuda", dtype=odt) for _ in range(nb)]
-    bias = [torch.randn(n, device="cuda") for _ in range(nb)] if obf else None
+    bias = [torch.randn(n, device="cuda") for _ in range(nb)] if obf and not NO_BIAS else None
     f = lambda: ops.gemm(A, B, C, m=m, n=n, k=k, lda=m if ak else (0 if lda_pad < 0 else (lda_pad or k)), ldb=n if bk else k, ldc=n, a_kouter=bool(ak),
                          b_kouter=bool(bk), dtype=dt, out_dtype=odt, bias=bias)
     f()
@@ -67,7 +70,9 @@ if __name__ == "__main__":
     ap.add_argument("--variants", default="", help="';'-separated option sets, each 'name=v,name=v' (tt_set_option); "
                                                    "'-' = defaults; rounds interleave the variants")
     ap.add_argument("--rounds", type=int, default=1)
+    ap.add_argument("--no-bias", action="store_true", help="no bias epilogue (e.g. option gemm_il)")
     a = ap.parse_args()
+    NO_BIAS = a.no_bias
     if a.regstage:
         os.environ["TT_GEMM_REGSTAGE"] = a.regstage
     if not a.variants:

@@ -1,5 +1,5 @@
 """tt_hardneg_topk (get_hard_negatives, enhanced_two_tower.py:123-133, batched) through the
-C ABI. bf16 with h in {128, 256} runs the streamed scan of tt_score.hip (chunk maxima ->
+C ABI. bf16 with h in {128, 256, 512} runs the streamed scan of tt_score.hip (chunk maxima ->
 exact chunk selection -> bit-identical rescoring -> top-k); other shapes run the GEMM +
 split top-k of tt_loss.hip. Integer-valued operands make every dot product exact in fp32
 whatever the summation order, so indices -- ties included, which go to the lower column
@@ -47,6 +47,8 @@ CASES = [  # B, nd, h, label_offset, k
     (257, 2000, 128, -1, 16),    # nothing masked (serving), k = 16
     (100, 200, 256, 0, 5),       # nch = 4 < k: every chunk selected
     (40, 70, 128, 3, 1),         # k = 1, two chunks
+    (300, 1000, 512, 0, 5),      # h 512 (configs[4]): 4-wave scan, 2-slot ring
+    (129, 4100, 512, 7, 16),     # h 512: partial row tile, odd tile count per split, k = 16
     (96, 640, 64, 0, 5),         # GEMM + split path (h = 64)
     (33, 999, 96, -1, 7),        # GEMM + split path (h = 96)
 ]
@@ -68,7 +70,7 @@ def test_hardneg_exact(dt, B, nd, h, lab, k):
     assert torch.equal(gv.double(), rv)
 
 
-@pytest.mark.parametrize("h", [128, 256])
+@pytest.mark.parametrize("h", [128, 256, 512])
 def test_hardneg_all_ties(h):
     """Every score equal: all chunk maxima tie, so the selection must take the lowest
     chunks and the result is the k lowest unmasked columns."""
@@ -102,7 +104,8 @@ def test_hardneg_bench_size_consistent():
     assert len(set(gi[0].tolist())) == k
 
 
-@pytest.mark.parametrize("B,nd,h,lab", [(1000, 3000, 256, 0), (300, 4100, 128, -1), (8192, 8192, 256, 0)])
+@pytest.mark.parametrize("B,nd,h,lab", [(1000, 3000, 256, 0), (300, 4100, 128, -1), (8192, 8192, 256, 0),
+                                         (1000, 3000, 512, 0), (8192, 8192, 512, 0)])
 def test_hardneg_scan_matches_gemm_path(B, nd, h, lab):
     """Random (non-integer) normalised bf16 rows: the streamed scan and the GEMM + split
     top-k path form every score with the same MFMA instruction and k order, so indices

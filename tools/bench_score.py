@@ -2,6 +2,7 @@
 the launching stream): hard-negative mining (tt_hardneg_topk) and the fused InfoNCE
 forward. Run under `rocprofv3 --kernel-trace --stats` for the per-kernel split."""
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -80,12 +81,23 @@ if __name__ == "__main__":
     ap.add_argument("--ops", default="hardneg,infonce")
     ap.add_argument("--hn-shapes", default="8192x8192x256,8192x65536x256,8192x8192x512",
                     help="hard-negative shapes B x N x h")
+    ap.add_argument("--variants", default="", help='hard-negative option sets, e.g. "wide=hn_wide=1;map=hn_map=1"')
     a = ap.parse_args()
     bf = torch.bfloat16
+    variants = [("default", {})]
+    for v in filter(None, a.variants.split(";")):
+        name, rest = v.split("=", 1)
+        variants.append((name, {kv.split("=")[0]: int(kv.split("=")[1]) for kv in rest.split(",")}))
     if "hardneg" in a.ops:
         for shp in a.hn_shapes.split(","):
             B, nd, h = (int(x) for x in shp.split("x"))
-            print(json.dumps(hardneg(B, nd, h, 5, bf, a.iters)), flush=True)
+            for name, opts in variants:
+                with contextlib.ExitStack() as es:
+                    for k, v in opts.items():
+                        es.enter_context(_lib.option(k, v))
+                    r = hardneg(B, nd, h, 5, bf, a.iters)
+                r["variant"] = name
+                print(json.dumps(r), flush=True)
     if "infonce" in a.ops:
         for B, nd, h in ((8192, 8192, 256), (8192, 65536, 256), (8192, 8192, 512)):
             print(json.dumps(infonce(B, nd, h, bf, a.iters)), flush=True)

@@ -29,12 +29,20 @@
 
 namespace {
 
-constexpr int SC_COLS = 64;                     // document columns per tile (= per chunk)
-constexpr int SC_WAVES = 8;                     // 512 threads: two waves per SIMD
-constexpr int SC_RB = 2;                        // 16-query MFMA blocks per wave
-constexpr int SC_ROWS = SC_WAVES * SC_RB * 16;  // 256 query rows per workgroup
-constexpr int SC_TPS_MAX = 32;                  // tiles per workgroup (chunk-max staging)
-constexpr int SC_SLOTS = 4;                     // LDS tile ring: two pairs of tiles
+constexpr int SC_COLS = 64;     // document columns per tile (= per chunk)
+constexpr int SC_RB = 2;        // 16-query MFMA blocks per wave
+constexpr int SC_TPS_MAX = 32;  // tiles per workgroup (chunk-max staging)
+
+// Per width (h = 32 KS). h <= 256: 8 waves (two per SIMD, 256 query rows per workgroup)
+// and a 4-slot LDS tile ring that travels in pairs. h 512: a tile is 64 KiB and the
+// query fragments alone are 128 registers per lane, so 4 waves (one per SIMD, 512
+// registers each, 128 query rows) and a 2-slot ring, one tile per barrier.
+template <int KS>
+struct ScanCfg {
+  static constexpr int WAVES = KS <= 8 ? 8 : 4;
+  static constexpr int ROWS = WAVES * SC_RB * 16;
+  static constexpr int SLOTS = KS <= 8 ? 4 : 2;
+};
 
 // max over the four 16-lane rows of a wave (lanes l, l+16, l+32, l+48), result in all
 TT_DEV float rowgroup_max4(float v) {
@@ -51,8 +59,8 @@ template <int KS>
 struct ScanTile {
   static constexpr int CPR = KS * 4;
   static constexpr int BYTES = SC_COLS * CPR * 16;
-  static constexpr int DPW = BYTES / 1024 / SC_WAVES;  // 1 KiB DMA instructions per wave
-  static_assert(DPW >= 1 && BYTES % (1024 * SC_WAVES) == 0, "tile/wave mismatch");
+  static constexpr int DPW = BYTES / 1024 / ScanCfg<KS>::WAVES;  // 1 KiB DMA instructions per wave
+  static_assert(DPW >= 1 && BYTES % (1024 * ScanCfg<KS>::WAVES) == 0, "tile/wave mismatch");
   TT_DEV static int off(int n, int c) { return (n * CPR + (c ^ (n & 15))) * 16; }
 };
 
@@ -99,12 +107,14 @@ TT_DEV uint4 ld_frag(const bf16_t* __restrict__ base, long row, long nrows, int 
 // Grid: row tiles x column splits, 1-D: block b -> split b % S (a split's workgroups
 // share one XCD label and its document slice stays in that L2), row tile b / S.
 template <int KS>
-__global__ __launch_bounds__(SC_WAVES * 64, 1) void hn_scan_kernel(const bf16_t* __restrict__ Q, long bq,
+__global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(const bf16_t* __restrict__ Q, long bq,
                                                                  const bf16_t* __restrict__ D, long nd,
                                                                  long label_off, int S, int tps, long nch,
                                                                  float* __restrict__ CM, int map) {
   using TI = ScanTile<KS>;
-  // 4 x 32 KiB tile ring + chunk maxima [tile][row]: all 160 KiB, one workgroup per CU
+  constexpr int SC_WAVES = ScanCfg<KS>::WAVES, SC_ROWS = ScanCfg<KS>::ROWS, SC_SLOTS = ScanCfg<KS>::SLOTS;
+  // tile ring + chunk maxima [tile][row]: 4 x 32 KiB + 32 KiB (h 256) or 2 x 64 KiB + 16
+  // KiB (h 512), one workgroup per CU
   __shared__ __attribute__((aligned(16))) char lds[SC_SLOTS * TI::BYTES + SC_TPS_MAX * SC_ROWS * 4];
   float* cms = reinterpret_cast<float*>(lds + SC_SLOTS * TI::BYTES);
   // map 0: blocks round-robin over the XCDs, so split b % S stays on one XCD and its
@@ -123,7 +133,7 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void hn_scan_kernel(const bf16_t*
   dm.init();
   const uint32_t lbase = __builtin_amdgcn_readfirstlane(ttg::lds_addr_of(lds));
   dm.issue(D, nd, t0 * SC_COLS, lbase);
-  if (nt > 1) dm.issue(D, nd, (t0 + 1) * SC_COLS, lbase + TI::BYTES);
+  if (SC_SLOTS == 4 && nt > 1) dm.issue(D, nd, (t0 + 1) * SC_COLS, lbase + TI::BYTES);
   uint4 qa[SC_RB][KS];
 #pragma unroll
   for (int qb = 0; qb < SC_RB; ++qb)
@@ -140,8 +150,14 @@ __global__ __launch_bounds__(SC_WAVES * 64, 1) void hn_scan_kernel(const bf16_t*
   // Tiles travel in pairs: at every even tile, one wait + barrier retires the pair (t, t+1)
   // for every wave and frees slots (t+2)%4, (t+3)%4 (last read before this barrier), into
   // which the next pair is requested; it lands while this pair is computed.
+  // With two slots (h 512) every tile is retired alone and the next one requested into
+  // the slot its predecessor freed.
   auto sync = [&](int t) {
-    if ((t & 1) == 0) {
+    if (SC_SLOTS == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (t + 1 < nt) dm.issue(D, nd, (t0 + t + 1) * SC_COLS, lbase + (uint32_t)((t + 1) % 2) * TI::BYTES);
+    } else if ((t & 1) == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       if (t + 2 < nt) dm.issue(D, nd, (t0 + t + 2) * SC_COLS, lbase + (uint32_t)((t + 2) % SC_SLOTS) * TI::BYTES);
@@ -281,7 +297,16 @@ __global__ __launch_bounds__(256) void hn_select_kernel(const float* __restrict_
   int li[KM];
   ttk::init<KM>(lv, li);
   const int nsel = (int)(nch < k ? nch : k);
-  for (long c = lane; c < nch; c += 64) ttk::insert<KM>(lv, li, nsel, CM[row * nch + c], (int)c);
+  // four loads in flight per lane before the inserts (nch is 128 at 8192 documents)
+  const float* cr = CM + row * nch;
+  for (long c0 = lane; c0 < nch; c0 += 4 * 64) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = c0 + u * 64 < nch ? cr[c0 + u * 64] : -FLT_MAX;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (c0 + u * 64 < nch) ttk::insert<KM>(lv, li, nsel, v[u], (int)(c0 + u * 64));
+  }
   float ov[KM];
   int oi[KM];
   ttk::wave_topk<KM>(lv, li, nsel, ov, oi);
@@ -292,7 +317,7 @@ __global__ __launch_bounds__(256) void hn_select_kernel(const float* __restrict_
 // Step 3: one workgroup per (chunk c, segment of RS_SEG rows). It collects the (row,
 // slot) entries of its segment that selected c (a scan of sel; LDS list), then its waves
 // rescore them 16 rows at a time with the MFMA orientation and k order of step 1: the
-// chunk's documents as A (registers), the gathered query rows as B. The segments bound
+// chunk's documents as A (staged in LDS), the gathered query rows as B. The segments bound
 // the work of one workgroup when every row selects the same chunks (correlated rows).
 constexpr int RS_SEG = 1024;
 constexpr int RS_THREADS = 512;
@@ -303,14 +328,26 @@ __global__ __launch_bounds__(RS_THREADS) void hn_rescore_kernel(const bf16_t* __
                                                          int nsel, const int32_t* __restrict__ sel,
                                                          float* __restrict__ cand) {
   constexpr int h = 32 * KS;
+  // the chunk's documents (64 x h bf16: 16 / 32 / 64 KiB) are staged in LDS, 16-byte
+  // chunk c of document n at slot c ^ (n & 15) so the 16-document fragment reads are
+  // conflict-free (held in registers instead, h 256 takes 207 registers per lane and
+  // measured 29.7 us at 8192 x 8192 for the rescoring against 22.1 at h 512 from LDS)
+  constexpr int CPD = 4 * KS;  // 16-byte chunks per document
   __shared__ int list[RS_SEG];  // a row selects a chunk at most once
   __shared__ int lcount;
+  __shared__ uint4 dimg[SC_COLS * CPD];
   const int c = blockIdx.x;
   const long n0 = (long)c * SC_COLS;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long seg = (long)blockIdx.y * RS_SEG;
   const long seg1 = seg + RS_SEG < bq ? seg + RS_SEG : bq;
   if (threadIdx.x == 0) lcount = 0;
+#pragma unroll
+  for (int q = 0; q < SC_COLS * CPD / RS_THREADS; ++q) {
+    const int i = threadIdx.x + q * RS_THREADS, n = i / CPD, cc = i % CPD;
+    dimg[n * CPD + (cc ^ (n & 15))] =
+        n0 + n < nd ? *reinterpret_cast<const uint4*>(D + (n0 + n) * h + cc * 8) : make_uint4(0, 0, 0, 0);
+  }
   __syncthreads();
   // the segment's entries, 4 per 16-byte load (seg * k is a multiple of 4)
   const int total = (int)(seg1 - seg) * k;
@@ -328,15 +365,12 @@ __global__ __launch_bounds__(RS_THREADS) void hn_rescore_kernel(const bf16_t* __
   __syncthreads();
   const int n = lcount;
   if (wave * 16 >= n) return;
-  uint4 fa[4][KS];
-#pragma unroll
-  for (int db = 0; db < 4; ++db)
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) fa[db][ks] = ld_frag(D, n0 + db * 16 + (lane & 15), nd, h, ks);
   for (int g = wave; g * 16 < n; g += RS_THREADS / 64) {
     const int ei = g * 16 + (lane & 15);
     const long e = ei < n ? seg * k + list[ei] : -1;
     const long row = e >= 0 ? e / k : bq;  // bq -> zero fragment
+    // keeps the LDS fragment reads inside the loop (hoisted, they would need 256 registers)
+    asm volatile("" ::: "memory");
     f32x4 acc[4];
 #pragma unroll
     for (int db = 0; db < 4; ++db) acc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -344,7 +378,11 @@ __global__ __launch_bounds__(RS_THREADS) void hn_rescore_kernel(const bf16_t* __
     for (int ks = 0; ks < KS; ++ks) {
       const uint4 qf = ld_frag(Q, row, bq, h, ks);
 #pragma unroll
-      for (int db = 0; db < 4; ++db) acc[db] = ttg::mma<bf16_t>(fa[db][ks], qf, acc[db]);
+      for (int db = 0; db < 4; ++db) {
+        const int dn = db * 16 + (lane & 15);
+        const uint4 df = dimg[dn * CPD + ((ks * 4 + (lane >> 4)) ^ (dn & 15))];
+        acc[db] = ttg::mma<bf16_t>(df, qf, acc[db]);
+      }
     }
     if (e >= 0) {
       float* dst = cand + e * SC_COLS;  // e = row * k + slot
@@ -376,10 +414,17 @@ __global__ __launch_bounds__(256) void hn_final_kernel(const float* __restrict__
   float lv[KM];
   int li[KM];
   ttk::init<KM>(lv, li);
-  for (int s = 0; s < nsel; ++s) {
-    const int col = sel[row * k + s] * SC_COLS + lane;
-    ttk::insert<KM>(lv, li, k, cand[(row * k + s) * SC_COLS + lane], col);
+  // every selected chunk's candidate and chunk id requested before the first insert
+  float cv[KM];
+  int cc[KM];
+#pragma unroll
+  for (int s = 0; s < KM; ++s) {
+    cv[s] = s < nsel ? cand[(row * k + s) * SC_COLS + lane] : -FLT_MAX;
+    cc[s] = s < nsel ? sel[row * k + s] : 0;
   }
+#pragma unroll
+  for (int s = 0; s < KM; ++s)
+    if (s < nsel) ttk::insert<KM>(lv, li, k, cv[s], cc[s] * SC_COLS + lane);
   float ov[KM];
   int oi[KM];
   ttk::wave_topk<KM>(lv, li, k, ov, oi);
@@ -398,10 +443,10 @@ struct HnPlan {
 
 long al256(long x) { return (x + 255) & ~255L; }
 
-HnPlan hn_plan(long bq, long nd, int k) {
+HnPlan hn_plan(long bq, long nd, int k, int rows) {
   HnPlan p{};
   p.nch = (nd + SC_COLS - 1) / SC_COLS;
-  p.RT = (bq + SC_ROWS - 1) / SC_ROWS;
+  p.RT = (bq + rows - 1) / rows;
   long S = (256 + p.RT - 1) / p.RT;
   const long smin = (p.nch + SC_TPS_MAX - 1) / SC_TPS_MAX;
   if (S < smin) S = smin;
@@ -417,12 +462,12 @@ HnPlan hn_plan(long bq, long nd, int k) {
 template <int KS>
 int hn_run(const bf16_t* qn, long bq, const bf16_t* dn, long nd, long label_offset, int k, int32_t* idx, float* val,
            char* ws, hipStream_t st) {
-  const HnPlan p = hn_plan(bq, nd, k);
+  const HnPlan p = hn_plan(bq, nd, k, ScanCfg<KS>::ROWS);
   float* CM = reinterpret_cast<float*>(ws);
   int32_t* sel = reinterpret_cast<int32_t*>(ws + p.off_sel);
   float* cand = reinterpret_cast<float*>(ws + p.off_cand);
   const int nsel = (int)(p.nch < k ? p.nch : k);
-  hipLaunchKernelGGL((hn_scan_kernel<KS>), dim3((unsigned)(p.RT * p.S)), dim3(SC_WAVES * 64), 0, st, qn, bq, dn, nd, label_offset, (int)p.S,
+  hipLaunchKernelGGL((hn_scan_kernel<KS>), dim3((unsigned)(p.RT * p.S)), dim3(ScanCfg<KS>::WAVES * 64), 0, st, qn, bq, dn, nd, label_offset, (int)p.S,
                      (int)p.tps, p.nch, CM, tt::opt(tt::OPT_HN_MAP));
   TT_CHECK_LAUNCH("hn_scan_kernel");
   const dim3 rows4((unsigned)tt_ceil_div(bq, 4));
@@ -444,14 +489,15 @@ int hn_run(const bf16_t* qn, long bq, const bf16_t* dn, long nd, long label_offs
 
 }  // namespace
 
-// Used by tt_hardneg_topk (tt_loss.hip) for bf16 operands with h in {128, 256}.
-long tt_hn_scan_ws_size(long bq, long nd, int k) { return hn_plan(bq, nd, k).bytes; }
+// Used by tt_hardneg_topk (tt_loss.hip) for bf16 operands with h in {128, 256, 512}.
+// The workspace does not depend on the rows per workgroup.
+long tt_hn_scan_ws_size(long bq, long nd, int k) { return hn_plan(bq, nd, k, ScanCfg<8>::ROWS).bytes; }
 
 // option hn_gemm = 1 forces the GEMM + split top-k path (tests compare the two bit-exactly:
 // both produce every score with the same MFMA instruction and k order).
 bool tt_hn_scan_supported(int dtype, int h) {
   const bool force_gemm = tt::opt(tt::OPT_HN_GEMM) == 1;
-  return !force_gemm && dtype == TT_BF16 && (h == 128 || h == 256);
+  return !force_gemm && dtype == TT_BF16 && (h == 128 || h == 256 || h == 512);
 }
 
 int tt_hn_scan_topk(const void* qn, long bq, const void* dn, long nd, int h, long label_offset, int k, int32_t* idx,
@@ -460,6 +506,7 @@ int tt_hn_scan_topk(const void* qn, long bq, const void* dn, long nd, int h, lon
   const bf16_t* d = static_cast<const bf16_t*>(dn);
   char* w = static_cast<char*>(ws);
   hipStream_t st = (hipStream_t)stream;
+  if (h == 512) return hn_run<16>(q, bq, d, nd, label_offset, k, idx, val, w, st);
   if (h == 256) return hn_run<8>(q, bq, d, nd, label_offset, k, idx, val, w, st);
   return hn_run<4>(q, bq, d, nd, label_offset, k, idx, val, w, st);
 }

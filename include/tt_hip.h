@@ -134,6 +134,12 @@ int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B, int T, in
  * H <= 512; 64 batch rows per workgroup kept resident for all T steps, hstate unused),
  * T for the per-step kernel (fp32, other H, or env TT_GRU_STEP=1). */
 int tt_gru_fwd_launches(int dtype, int T, int H);
+/* bf16, H 256 / 512, batch large enough (or option gru_fwd_xc = 2): tt_gru_fwd runs the
+ * column-split persistent kernel instead (H/64 workgroups share a block of batch rows, each
+ * keeps 64 units' W_hh rows in registers; h is exchanged between them every step through
+ * an internal per-device workspace, so one such forward per device at a time). Reports
+ * and clears its wait-timeout flag (1: some launch's outputs are invalid); synchronises. */
+int tt_gru_fwd_xc_status(int* timed_out);
 
 /* Backward (BPTT) of tt_gru_fwd. Produces dL/dg (= dgx, feeds dWih, dbih and the
  * layer-input gradient) and dL/dgh (feeds dWhh), plus per-tile bias partial sums

@@ -15,6 +15,8 @@ Both kernels run the same MFMA sequence along K and the same fp32 gate expressio
 every output is expected bit-identical; the fraction of differing elements and the
 largest difference in bf16 ulps are printed.
 """
+import ctypes
+
 import pytest
 import torch
 
@@ -118,13 +120,41 @@ def _assert_equivalent(outs_p, outs_s, B, T, H, bhn):
     assert not bad, f"persistent vs per-step forward differ: {bad}"
 
 
-def test_bench_grid_persistent_forward_matches_per_step():
+def _xc_timed_out():
+    flag = ctypes.c_int(0)
+    call("tt_gru_fwd_xc_status", ctypes.byref(flag))
+    return flag.value
+
+
+@pytest.mark.parametrize("xc", [0, 1])
+def test_bench_grid_persistent_forward_matches_per_step(xc):
     """configs[2] layer-0 shape: B 8192, T 64, H 512, 2 towers x 2 directions in one
-    launch, dropout 0.1 on the X1 copy: gru_fwd_seq<4,8> vs T launches of gru_fwd_step."""
+    launch, dropout 0.1 on the X1 copy: the persistent forward (xc 1: the column-split
+    gru_fwd_xc the bench runs; xc 0: the row-owning gru_fwd_seq<4,8>) vs T launches of
+    gru_fwd_step."""
     B, T, H, ntow = 8192, 64, 512, 2
     G, whh, bhn = _inputs(ntow, B, T, H, seed=3)
     outs_s = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=1)
-    outs_p = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=0)
+    with option("gru_fwd_xc", xc):
+        outs_p = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=0)
+    assert _xc_timed_out() == 0
+    _assert_equivalent(outs_p, outs_s, B, T, H, bhn)
+
+
+@pytest.mark.parametrize("H,B,T,ntow", [(512, 1000, 12, 2), (256, 1000, 12, 2), (512, 3000, 5, 2), (512, 70, 3, 2),
+                                        (256, 64, 1, 2), (512, 5000, 7, 1), (256, 8192, 4, 2), (512, 300, 2, 1)])
+def test_column_split_forward_matches_per_step(H, B, T, ntow):
+    """gru_fwd_xc forced (option gru_fwd_xc = 2) wherever it applies: the H/64 member
+    workgroups of a group exchange h through write-through stores / loads every step.
+    Rows per group that are not a multiple of the 256-row round (B 3000 over 8 groups per
+    recurrence: 375 = 256 + 119), groups with no rows at all (B 70, B 64), one tower
+    (two recurrences: 16 groups each) and T = 1; same MFMA k order and gate arithmetic as
+    the per-step kernel, so every output is bit-identical."""
+    G, whh, bhn = _inputs(ntow, B, T, H, seed=11 * H + B + T + ntow)
+    outs_s = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=1)
+    with option("gru_fwd_xc", 2):
+        outs_p = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=0)
+    assert _xc_timed_out() == 0
     _assert_equivalent(outs_p, outs_s, B, T, H, bhn)
 
 

@@ -37,7 +37,7 @@ constexpr OptDef kOpts[OPT_N] = {
     {"infonce_flash", "TT_INFONCE_FLASH", 1},     {"gru_fwd_rr", "TT_GRU_FWD_RR", 0},
     {"gru_fwd_wr", "TT_GRU_FWD_WR", 0},           {"hn_map", "TT_HN_MAP", 0},
     {"gemm_skew", "TT_GEMM_SKEW", 0},             {"gemm_persist_maxk", "TT_GEMM_PERSIST_MAXK", 24},
-    {"gru_fwd_pair", "TT_GRU_FWD_PAIR", 0},
+    {"gru_fwd_pair", "TT_GRU_FWD_PAIR", 0},       {"gru_fwd_xc", "TT_GRU_FWD_XC", 1},
 };
 struct OptTable {
   std::atomic<int> v[OPT_N];

@@ -2238,6 +2238,298 @@ __global__ __launch_bounds__(wr::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
   __builtin_amdgcn_s_barrier();
 }
 
+// ---- column-split persistent forward (gru_fwd_xc, bf16, H 256 / 512) ----------------
+// Every other forward here gives a workgroup a set of batch rows and all 3H gate columns,
+// so each workgroup re-streams the whole W_hh (1.5 MiB at H 512) from L2 at every step:
+// that stream, ~30 GB/s into a CU, is what bounds gru_fwd_seq. Here the
+// split is the other way round. A group of M = H/64 workgroups (one per CU, all on one XCD
+// under round-robin placement -- speed only, never correctness) shares a block of batch
+// rows; member m owns hidden units [64m, 64m+64) and keeps its 192 W_hh rows (r, z, n of
+// those units; 192 KiB at H 512) in the accumulator registers of its 4 waves for the whole
+// launch. Per step the members exchange h instead: each writes its 64 units of h_s for the
+// block's rows to a group image (16-byte write-through stores), drains, and bumps the
+// group's arrival counter; before step s+1 every member waits for all M arrivals and reads
+// the full h_s rows back (16-byte write-through loads, so no L1 line can be stale:
+// cdna_hip_programming.md §6 Guideline 16 / MI355X_MICROARCH.md, hand-off table row 1).
+// That is H*2 bytes of L2 traffic per row and step instead of the whole W_hh per 64 rows.
+//   rows : the group's rows run in rounds of RR = 256 (fp32 state of a round in LDS), each
+//          round in chunks of 32 rows: h chunk -> LDS (double-buffered) -> MFMA
+//          (acc = C^T: 4 consecutive units of one row per lane) -> gates staged in LDS ->
+//          every thread updates 8 consecutive units of one row with 16-byte G / Y / S / X1
+//          accesses (full 128-byte lines per row and member)
+//   order: the MFMAs of chunk c+1 are issued ahead of chunk c's gate arithmetic, so the
+//          matrix pipe and the VALU run side by side in each wave
+// Same MFMA sequence along k (K-steps of 32 in order, from zero) and the same gru_cell as
+// the per-step kernel, so every output is bit-identical to it (tests/test_gpu_gru_persistent.py).
+// Needs all groups resident at once: one workgroup per CU (the LDS use forbids two), grid =
+// 8 * M * (CUs / 8M) <= CUs; every wait is bounded (timeout flag, tt_gru_fwd_xc_status).
+typedef __attribute__((address_space(1))) unsigned xc_gu32;
+namespace xc {
+constexpr int NT = 256;                // 4 waves, one per SIMD
+constexpr int CR = 32;                 // batch rows per chunk (8 epilogue threads per row)
+constexpr int RR = 256;                // batch rows per round
+constexpr int NCH = RR / CR;           // chunks per round
+constexpr int SSTR = 68;               // LDS fp32 state row stride (64 units + 16 B pad)
+constexpr int STG = CR * 192 * 4;      // gate staging [32 rows][192 columns] fp32
+constexpr int CSTR = 32;               // arrival counters 128 B apart
+constexpr unsigned OOB = 0x80000000u;  // buffer offset past num_records: load 0 / store dropped
+template <int H>
+struct Cfg {
+  static constexpr int M = H / 64;         // members per group
+  static constexpr int NKT = H / 32;       // MFMA K-steps
+  static constexpr int QPW = H / 64;       // 1-KiB h pieces per wave and chunk
+  static constexpr int SLOT = CR * H * 2;  // h chunk image: [K-step][row block][16 B x 64 lanes]
+  static constexpr int ST = RR * SSTR * 4;
+  static constexpr int LDS = ST + 2 * SLOT + STG;
+};
+static_assert(Cfg<512>::LDS <= 163840 && Cfg<256>::LDS <= 163840, "gru_fwd_xc LDS budget");
+}  // namespace xc
+
+struct XcWs {
+  bf16_t* xb;     // [groups][2][RR][H] h exchange images (parity = step index & 1)
+  unsigned* cnt;  // [groups][CSTR] arrival counters, zeroed before every launch
+  unsigned* err;  // set on a wait timeout
+  int qg;         // groups per XCD
+  int nrec;       // recurrences (groups are dealt to them round-robin)
+  int rpg;        // batch rows per group
+  int nround;     // rounds of RR rows per group
+};
+
+TT_DEV void xc_wait(xc_gu32* cnt, unsigned target, xc_gu32* err) {
+  for (unsigned spins = 0;; ++spins) {
+    if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return;
+    if ((spins & 1023u) == 1023u) {
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
+      if (spins > (1u << 22)) {  // several seconds: a member never arrived
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// h rows [32c, 32c+32) of an exchange image -> registers (write-through loads): piece p of
+// wave w is K-step kt, row block rb of the chunk image, one 16-byte MFMA fragment per lane
+template <int H>
+TT_DEV void xc_load_h(__amdgpu_buffer_rsrc_t rx, int c, tt_u32x4 (&hv)[xc::Cfg<H>::QPW]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int p = 0; p < xc::Cfg<H>::QPW; ++p) {
+    const int q = w * xc::Cfg<H>::QPW + p, kt = q >> 1, rb = q & 1;
+    const int row = c * xc::CR + rb * 16 + (lane & 15), k0 = kt * 32 + (lane >> 4) * 8;
+    hv[p] = __builtin_amdgcn_raw_buffer_load_b128(rx, (row * H + k0) * 2, 0, 16);
+  }
+}
+template <int H>
+TT_DEV void xc_put_h(char* slot, const tt_u32x4 (&hv)[xc::Cfg<H>::QPW]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int p = 0; p < xc::Cfg<H>::QPW; ++p)
+    *reinterpret_cast<tt_u32x4*>(slot + (w * xc::Cfg<H>::QPW + p) * 1024 + lane * 16) = hv[p];
+}
+// gh^T of the chunk's 32 rows x this wave's 48 gate columns (16 units x r, z, n)
+template <int H>
+TT_DEV void xc_mfma(const char* slot, const tt_u32x4 (&wa)[3][xc::Cfg<H>::NKT], f32x4 (&acc)[2][3]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int g = 0; g < 3; ++g) acc[rb][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kt = 0; kt < xc::Cfg<H>::NKT; ++kt)
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const tt_u32x4 hf = *reinterpret_cast<const tt_u32x4*>(slot + (kt * 2 + rb) * 1024 + lane * 16);
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+        acc[rb][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8v, wa[g][kt]),
+                                                             __builtin_bit_cast(bf16x8v, hf), acc[rb][g], 0, 0, 0);
+    }
+}
+TT_DEV void xc_stage(float* stg, const f32x4 (&acc)[2][3]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+      *reinterpret_cast<f32x4*>(stg + stg_off(rb * 16 + (lane & 15), g * 64 + 16 * w + 4 * (lane >> 4))) = acc[rb][g];
+}
+
+template <int H>
+__global__ __launch_bounds__(xc::NT, 1) void gru_fwd_xc(FwdArgs a, XcWs ws) {
+  using C = xc::Cfg<H>;
+  constexpr int M = C::M;
+  __shared__ __attribute__((aligned(16))) char lds[C::LDS];
+  float* stt = reinterpret_cast<float*>(lds);
+  char* slots = lds + C::ST;
+  float* stg = reinterpret_cast<float*>(lds + C::ST + 2 * C::SLOT);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // group / member: blocks b and b + 8 share an XCD under round-robin placement
+  const int xcd = blockIdx.x & 7, jj = blockIdx.x >> 3;
+  const int grp = xcd * ws.qg + jj / M, mem = jj % M;
+  const int rz = grp % ws.nrec, gi = grp / ws.nrec;
+  const FwdRec R = a.r[rz];
+  const int T_ = a.T, B = a.B;
+  const int gb0 = gi * ws.rpg;  // first batch row of the group
+  xc_gu32* cnt = (xc_gu32*)(uintptr_t)(ws.cnt + grp * xc::CSTR);
+  xc_gu32* err = (xc_gu32*)(uintptr_t)ws.err;
+  bf16_t* xbg = ws.xb + (long)grp * 2 * xc::RR * H;
+  const __amdgpu_buffer_rsrc_t rx[2] = {tt_rsrc(xbg), tt_rsrc(xbg + xc::RR * H)};
+
+  // this wave's W_hh rows: A operand of gate g, K-step kt = rows g*H + 64 mem + 16 wave +
+  // (lane & 15), k = 32 kt + 8 (lane >> 4) .. +7; kept in accumulator registers
+  tt_u32x4 wa[3][C::NKT];
+  {
+    const bf16_t* W = static_cast<const bf16_t*>(R.whh);
+    // all loads first (one wait), then the moves into the accumulator file
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int kt = 0; kt < C::NKT; ++kt)
+        wa[g][kt] = *reinterpret_cast<const tt_u32x4*>(
+            W + (long)(g * H + 64 * mem + 16 * wave + (lane & 15)) * H + kt * 32 + (lane >> 4) * 8);
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int kt = 0; kt < C::NKT; ++kt) asm volatile("" : "+a"(wa[g][kt]));
+  }
+  // epilogue ownership: chunk row cr, units j .. j+7 of this member's 64
+  const int cr = tid >> 3, u0 = (tid & 7) * 8, j = 64 * mem + u0;
+  float bn[8];
+  {
+    const float4 b0 = *reinterpret_cast<const float4*>(R.bhn + j);
+    const float4 b1 = *reinterpret_cast<const float4*>(R.bhn + j + 4);
+    bn[0] = b0.x; bn[1] = b0.y; bn[2] = b0.z; bn[3] = b0.w;
+    bn[4] = b1.x; bn[5] = b1.y; bn[6] = b1.z; bn[7] = b1.w;
+  }
+  const bf16_t* G = static_cast<const bf16_t*>(R.g);
+  bf16_t* Yw = static_cast<bf16_t*>(R.y);
+  bf16_t* X1 = static_cast<bf16_t*>(R.x1);
+  bf16_t* S = static_cast<bf16_t*>(R.save);
+  const bool drop = X1 && a.drop_thresh;
+
+  int idx = 0;  // step counter over all rounds: parity of the exchange image, counter target
+  for (int r = 0; r < ws.nround; ++r) {
+    const int rb0 = gb0 + r * xc::RR;  // first batch row of the round
+    const int nrow = min(min(ws.rpg - r * xc::RR, xc::RR), B - rb0);  // rows of this round (may be <= 0)
+    const bool on = nrow > 0;
+    const long r0w = (long)(on ? rb0 : 0) * T_;
+    const __amdgpu_buffer_rsrc_t rG = tt_rsrc_n(G + r0w * a.ldg, on);
+    const __amdgpu_buffer_rsrc_t rY = tt_rsrc_n(Yw + r0w * a.ldy, on);
+    const __amdgpu_buffer_rsrc_t rX1 = tt_rsrc_n(X1 ? X1 + r0w * a.ldy : Yw, on && X1 != nullptr);
+    const __amdgpu_buffer_rsrc_t rS = tt_rsrc_n(S + r0w * 4L * H, on);
+    for (int i = tid; i < xc::RR * xc::SSTR / 4; i += xc::NT)
+      reinterpret_cast<float4*>(stt)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // gate inputs of chunk c at step s: 3 x 16 bytes per thread, issued a chunk ahead
+    auto load_g = [&](int s, int c, tt_u32x4 (&gx)[3]) {
+      const int t = R.dir ? T_ - 1 - s : s;
+      const int rr = c * xc::CR + cr;
+      const uint32_t og = rr < nrow ? (uint32_t)((rr * T_ + t) * (int)a.ldg + j) * 2u : xc::OOB;
+#pragma unroll
+      for (int g = 0; g < 3; ++g) gx[g] = __builtin_amdgcn_raw_buffer_load_b128(rG, (int)og, g * H * 2, 0);
+    };
+    tt_u32x4 gcur[3], gnxt[3];
+    load_g(0, 0, gcur);
+    for (int s = 0; s < T_; ++s, ++idx) {
+      const int t = R.dir ? T_ - 1 - s : s;
+      const bool mm = s > 0;  // h_{-1} = 0: the first step has no recurrent term
+      // all members finished step idx-1: its h is complete, and nobody still reads the
+      // image this step overwrites (written two steps ago)
+      if (idx > 0 && tid == 0) xc_wait(cnt, (unsigned)(M * idx), err);
+      __syncthreads();
+      const __amdgpu_buffer_rsrc_t rsrc_h = rx[(idx - 1) & 1];
+      const __amdgpu_buffer_rsrc_t rdst_h = rx[idx & 1];
+      tt_u32x4 hv[C::QPW];
+      f32x4 acc[2][3];
+      if (mm) {
+        xc_load_h<H>(rsrc_h, 0, hv);
+        xc_put_h<H>(slots, hv);
+        xc_load_h<H>(rsrc_h, 1, hv);
+      }
+      __syncthreads();
+      if (mm) {
+        xc_mfma<H>(slots, wa, acc);
+        xc_put_h<H>(slots + C::SLOT, hv);
+        xc_load_h<H>(rsrc_h, 2, hv);
+      } else {
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+          for (int g = 0; g < 3; ++g) acc[rb][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      xc_stage(stg, acc);
+      __syncthreads();
+#pragma unroll
+      for (int c = 0; c < xc::NCH; ++c) {
+        if (c + 1 < xc::NCH) {
+          load_g(s, c + 1, gnxt);
+          if (mm) xc_mfma<H>(slots + ((c + 1) & 1) * C::SLOT, wa, acc);
+        }
+        // ---- gate arithmetic of chunk c
+        {
+          const int rr = c * xc::CR + cr;
+          const bool ok = rr < nrow;
+          float xr[8], xz[8], xn[8], lr[8], lz[8], ln[8], hp[8], y[8], sr[8], sz[8], sn[8], sg[8];
+          unpack8(make_uint4(gcur[0][0], gcur[0][1], gcur[0][2], gcur[0][3]), xr);
+          unpack8(make_uint4(gcur[1][0], gcur[1][1], gcur[1][2], gcur[1][3]), xz);
+          unpack8(make_uint4(gcur[2][0], gcur[2][1], gcur[2][2], gcur[2][3]), xn);
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const float4 v0 = *reinterpret_cast<const float4*>(stg + stg_off(cr, 0 * 64 + u0 + 4 * h));
+            const float4 v1 = *reinterpret_cast<const float4*>(stg + stg_off(cr, 1 * 64 + u0 + 4 * h));
+            const float4 v2 = *reinterpret_cast<const float4*>(stg + stg_off(cr, 2 * 64 + u0 + 4 * h));
+            const float4 p = *reinterpret_cast<const float4*>(stt + rr * xc::SSTR + u0 + 4 * h);
+            lr[4 * h] = v0.x; lr[4 * h + 1] = v0.y; lr[4 * h + 2] = v0.z; lr[4 * h + 3] = v0.w;
+            lz[4 * h] = v1.x; lz[4 * h + 1] = v1.y; lz[4 * h + 2] = v1.z; lz[4 * h + 3] = v1.w;
+            ln[4 * h] = v2.x; ln[4 * h + 1] = v2.y; ln[4 * h + 2] = v2.z; ln[4 * h + 3] = v2.w;
+            hp[4 * h] = p.x; hp[4 * h + 1] = p.y; hp[4 * h + 2] = p.z; hp[4 * h + 3] = p.w;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            gru_cell(xr[e], xz[e], xn[e], lr[e], lz[e], ln[e], bn[e], hp[e], y[e], sr[e], sz[e], sn[e], sg[e]);
+          *reinterpret_cast<float4*>(stt + rr * xc::SSTR + u0) = make_float4(y[0], y[1], y[2], y[3]);
+          *reinterpret_cast<float4*>(stt + rr * xc::SSTR + u0 + 4) = make_float4(y[4], y[5], y[6], y[7]);
+          const uint4 yb = pack8bf(y);
+          st16_buf_sc1(rdst_h, (uint32_t)(rr * H + j) * 2u, 0, yb);  // the exchange image (all rows)
+          const int lrow = rr * T_ + t;
+          const uint32_t oy = ok ? (uint32_t)(lrow * (int)a.ldy + j) * 2u : xc::OOB;
+          const uint32_t os = ok ? (uint32_t)(lrow * 4 * H + j) * 2u : xc::OOB;
+          st16_buf(rY, oy, 0, yb);
+          st16_buf(rS, os, 0, pack8bf(sr));
+          st16_buf(rS, os, 2 * H, pack8bf(sz));
+          st16_buf(rS, os, 4 * H, pack8bf(sn));
+          st16_buf(rS, os, 6 * H, pack8bf(sg));
+          if (drop) {
+            const uint32_t grow = (uint32_t)(rb0 + rr) * (uint32_t)T_ + (uint32_t)t;
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              y[e] *= tt_dropout_scale(R.seed, R.row0 + grow, (uint32_t)(R.col0 + j + e), a.drop_thresh, a.inv_keep);
+          }
+          st16_buf(rX1, oy, 0, pack8bf(y));
+        }
+        if (mm && c + 2 < xc::NCH) {
+          xc_put_h<H>(slots + (c & 1) * C::SLOT, hv);  // chunk c+2 into the slot chunk c used
+          if (c + 3 < xc::NCH) xc_load_h<H>(rsrc_h, c + 3, hv);
+        }
+        __syncthreads();
+        if (c + 1 < xc::NCH) {
+          xc_stage(stg, acc);
+          __syncthreads();
+#pragma unroll
+          for (int g = 0; g < 3; ++g) gcur[g] = gnxt[g];
+        }
+      }
+      // publish h_s: every wave drains its stores (the exchange stores are write-through),
+      // then one lane counts the workgroup in
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (s + 1 < T_) load_g(s + 1, 0, gcur);
+    }
+  }
+}
+
 #ifdef TT_DIAG
 }  // namespace
 extern "C" int tt_diag_fwd_prof(unsigned long long* out) {  // [2048][8] host buffer
@@ -2311,6 +2603,105 @@ static int side_stream(SideStream** out) {
   return 0;
 }
 
+// gru_fwd_xc workspace per device: exchange images, arrival counters and the timeout flag,
+// allocated on first use under a mutex (one column-split forward per device at a time: a
+// second host thread on another stream would share the counters).
+struct XcDev {
+  int cus = 0;
+  size_t xb_bytes = 0;
+  bf16_t* xb = nullptr;
+  unsigned* cnt = nullptr;  // [512 groups][CSTR] + the timeout flag after them
+};
+static std::mutex g_xc_mu;
+static XcDev g_xc[64];
+constexpr int XC_MAX_GROUPS = 512;
+
+// Launch geometry of the column-split forward, or false where it does not apply.
+static bool xc_geometry(int dtype, int H, int nrec, int B, int T, long ldg, long ldy, int cus, XcWs& w, int& grid) {
+  const int v = tt::opt(tt::OPT_GRU_FWD_XC);
+  if (v == 0 || dtype != TT_DT_BF16 || (H != 512 && H != 256)) return false;
+  if (tt::opt(tt::OPT_GRU_STEP) == 1 || tt::opt(tt::OPT_GRU_FWD_RR) || tt::opt(tt::OPT_GRU_FWD_WR) ||
+      tt::opt(tt::OPT_GRU_FWD_PAIR))
+    return false;
+  const int M = H / 64;
+  const int qg = cus / (8 * M);
+  const int ng = 8 * qg;
+  if (qg < 1 || ng > XC_MAX_GROUPS || ng % nrec != 0) return false;
+  const int gpr = ng / nrec;
+  // auto mode: only where every group gets at least half a round of rows
+  if (v == 1 && (long)B < (long)gpr * (xc::RR / 2)) return false;
+  // per-round resources: byte offsets of RR rows x T steps stay below 2 GiB
+  if ((long)xc::RR * T * std::max({4L * H, ldy, ldg}) * 2 >= (1L << 31)) return false;
+  w.qg = qg;
+  w.nrec = nrec;
+  w.rpg = tt_ceil_div(B, gpr);
+  w.nround = tt_ceil_div(w.rpg, xc::RR);
+  grid = ng * M;
+  return true;
+}
+
+static int xc_device(XcDev** out) {
+  int dev = 0;
+  TT_CHECK_HIP(hipGetDevice(&dev));
+  TT_CHECK_ARG(dev >= 0 && dev < 64, "tt_gru_fwd: device %d", dev);
+  std::lock_guard<std::mutex> lock(g_xc_mu);
+  XcDev& x = g_xc[dev];
+  if (!x.cus) {
+    TT_CHECK_HIP(hipDeviceGetAttribute(&x.cus, hipDeviceAttributeMultiprocessorCount, dev));
+    TT_CHECK_HIP(hipMalloc(reinterpret_cast<void**>(&x.cnt), sizeof(unsigned) * (XC_MAX_GROUPS * xc::CSTR + 64)));
+    TT_CHECK_HIP(hipMemset(x.cnt, 0, sizeof(unsigned) * (XC_MAX_GROUPS * xc::CSTR + 64)));
+  }
+  *out = &x;
+  return 0;
+}
+
+// Timeout flag of the column-split forward on the current device (1 = a wait gave up: the
+// outputs of that launch are invalid); clears it. Synchronises the device.
+extern "C" int tt_gru_fwd_xc_status(int* timed_out) {
+  TT_CHECK_ARG(timed_out, "tt_gru_fwd_xc_status: null");
+  XcDev* x = nullptr;
+  TT_PROPAGATE(xc_device(&x));
+  TT_CHECK_HIP(hipDeviceSynchronize());
+  unsigned* flag = x->cnt + XC_MAX_GROUPS * xc::CSTR;
+  unsigned v = 0;
+  TT_CHECK_HIP(hipMemcpy(&v, flag, sizeof(v), hipMemcpyDeviceToHost));
+  TT_CHECK_HIP(hipMemset(flag, 0, sizeof(unsigned)));
+  *timed_out = v != 0;
+  return 0;
+}
+
+static int gru_fwd_xc_launch(const FwdArgs& a, int nrec, int B, int T, int H, long ldg, long ldy, hipStream_t st,
+                             bool* used) {
+  *used = false;
+  if (tt::opt(tt::OPT_GRU_FWD_XC) == 0 || (H != 512 && H != 256)) return 0;
+  XcDev* x = nullptr;
+  TT_PROPAGATE(xc_device(&x));
+  XcWs w{};
+  int grid = 0;
+  if (!xc_geometry(TT_DT_BF16, H, nrec, B, T, ldg, ldy, x->cus, w, grid)) return 0;
+  const int ng = grid / (H / 64);
+  {
+    std::lock_guard<std::mutex> lock(g_xc_mu);
+    const size_t need = (size_t)ng * 2 * xc::RR * H * sizeof(bf16_t);
+    if (x->xb_bytes < need) {
+      if (x->xb) TT_CHECK_HIP(hipFree(x->xb));
+      x->xb = nullptr;
+      x->xb_bytes = 0;
+      TT_CHECK_HIP(hipMalloc(reinterpret_cast<void**>(&x->xb), need));
+      x->xb_bytes = need;
+    }
+  }
+  w.xb = x->xb;
+  w.cnt = x->cnt;
+  w.err = x->cnt + XC_MAX_GROUPS * xc::CSTR;
+  TT_CHECK_HIP(hipMemsetAsync(x->cnt, 0, sizeof(unsigned) * ng * xc::CSTR, st));
+  if (H == 512) hipLaunchKernelGGL(gru_fwd_xc<512>, dim3(grid), dim3(xc::NT), 0, st, a, w);
+  else hipLaunchKernelGGL(gru_fwd_xc<256>, dim3(grid), dim3(xc::NT), 0, st, a, w);
+  TT_CHECK_LAUNCH("gru_fwd_xc");
+  *used = true;
+  return 0;
+}
+
 extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B, int T, int H, long ldg,
                           long ldy, float drop_p, void* stream) {
   TT_CHECK_ARG(dtype == TT_DT_F32 || dtype == TT_DT_BF16, "tt_gru_fwd: bad dtype");
@@ -2336,6 +2727,11 @@ extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B
   if (const char* e = getenv("TT_GRU_DBG")) a.dbg = atoi(e);
 #endif
   hipStream_t st = (hipStream_t)stream;
+  if (dtype == TT_DT_BF16) {
+    bool used = false;
+    TT_PROPAGATE(gru_fwd_xc_launch(a, nrec, B, T, H, ldg, ldy, st, &used));
+    if (used) return 0;
+  }
   if (gru_fwd_rr_ok(dtype, H)) {
     const dim3 grid(tt_ceil_div(B, 65536 / H) * nrec);
     const int v = tt::opt(tt::OPT_GRU_FWD_RR);

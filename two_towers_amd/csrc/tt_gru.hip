@@ -2264,6 +2264,9 @@ __global__ __launch_bounds__(wr::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
 // Needs all groups resident at once: one workgroup per CU (the LDS use forbids two), grid =
 // 8 * M * (CUs / 8M) <= CUs; every wait is bounded (timeout flag, tt_gru_fwd_xc_status).
 typedef __attribute__((address_space(1))) unsigned xc_gu32;
+#ifndef XC_VALU_PER_MFMA
+#define XC_VALU_PER_MFMA 2
+#endif
 namespace xc {
 constexpr int NT = 256;                // 4 waves, one per SIMD
 constexpr int CR = 32;                 // batch rows per chunk (8 epilogue threads per row)
@@ -2311,15 +2314,22 @@ TT_DEV void xc_wait(xc_gu32* cnt, unsigned target, xc_gu32* err) {
 
 // h rows [32c, 32c+32) of an exchange image -> registers (write-through loads): piece p of
 // wave w is K-step kt, row block rb of the chunk image, one 16-byte MFMA fragment per lane
+// (per-piece lane offsets ho[p] computed once; the chunk offset is a constant)
 template <int H>
-TT_DEV void xc_load_h(__amdgpu_buffer_rsrc_t rx, int c, tt_u32x4 (&hv)[xc::Cfg<H>::QPW]) {
+TT_DEV void xc_h_offsets(uint32_t (&ho)[xc::Cfg<H>::QPW]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int p = 0; p < xc::Cfg<H>::QPW; ++p) {
     const int q = w * xc::Cfg<H>::QPW + p, kt = q >> 1, rb = q & 1;
-    const int row = c * xc::CR + rb * 16 + (lane & 15), k0 = kt * 32 + (lane >> 4) * 8;
-    hv[p] = __builtin_amdgcn_raw_buffer_load_b128(rx, (row * H + k0) * 2, 0, 16);
+    ho[p] = (uint32_t)(((rb * 16 + (lane & 15)) * H + kt * 32 + (lane >> 4) * 8) * 2);
   }
+}
+template <int H>
+TT_DEV void xc_load_h(__amdgpu_buffer_rsrc_t rx, const uint32_t (&ho)[xc::Cfg<H>::QPW], int c,
+                      tt_u32x4 (&hv)[xc::Cfg<H>::QPW]) {
+#pragma unroll
+  for (int p = 0; p < xc::Cfg<H>::QPW; ++p)
+    hv[p] = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)ho[p], c * xc::CR * H * 2, 16);
 }
 template <int H>
 TT_DEV void xc_put_h(char* slot, const tt_u32x4 (&hv)[xc::Cfg<H>::QPW]) {
@@ -2328,24 +2338,35 @@ TT_DEV void xc_put_h(char* slot, const tt_u32x4 (&hv)[xc::Cfg<H>::QPW]) {
   for (int p = 0; p < xc::Cfg<H>::QPW; ++p)
     *reinterpret_cast<tt_u32x4*>(slot + (w * xc::Cfg<H>::QPW + p) * 1024 + lane * 16) = hv[p];
 }
-// gh^T of the chunk's 32 rows x this wave's 48 gate columns (16 units x r, z, n)
+// gh^T of the chunk's 32 rows x this wave's 48 gate columns (16 units x r, z, n); the
+// fragments of K-step kt+2 are requested before the MFMAs of kt (LDS latency off the chain)
 template <int H>
 TT_DEV void xc_mfma(const char* slot, const tt_u32x4 (&wa)[3][xc::Cfg<H>::NKT], f32x4 (&acc)[2][3]) {
+  constexpr int NKT = xc::Cfg<H>::NKT;
   const int lane = threadIdx.x & 63;
+  auto frag = [&](int kt, int rb) {
+    return *reinterpret_cast<const tt_u32x4*>(slot + (kt * 2 + rb) * 1024 + lane * 16);
+  };
 #pragma unroll
   for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
     for (int g = 0; g < 3; ++g) acc[rb][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+  tt_u32x4 f[3][2];
+  f[0][0] = frag(0, 0); f[0][1] = frag(0, 1);
+  f[1][0] = frag(1, 0); f[1][1] = frag(1, 1);
 #pragma unroll
-  for (int kt = 0; kt < xc::Cfg<H>::NKT; ++kt)
+  for (int kt = 0; kt < NKT; ++kt) {
+    if (kt + 2 < NKT) {
+      f[(kt + 2) % 3][0] = frag(kt + 2, 0);
+      f[(kt + 2) % 3][1] = frag(kt + 2, 1);
+    }
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb) {
-      const tt_u32x4 hf = *reinterpret_cast<const tt_u32x4*>(slot + (kt * 2 + rb) * 1024 + lane * 16);
+    for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
       for (int g = 0; g < 3; ++g)
         acc[rb][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8v, wa[g][kt]),
-                                                             __builtin_bit_cast(bf16x8v, hf), acc[rb][g], 0, 0, 0);
-    }
+                                                             __builtin_bit_cast(bf16x8v, f[kt % 3][rb]), acc[rb][g], 0, 0, 0);
+  }
 }
 TT_DEV void xc_stage(float* stg, const f32x4 (&acc)[2][3]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -2356,8 +2377,8 @@ TT_DEV void xc_stage(float* stg, const f32x4 (&acc)[2][3]) {
       *reinterpret_cast<f32x4*>(stg + stg_off(rb * 16 + (lane & 15), g * 64 + 16 * w + 4 * (lane >> 4))) = acc[rb][g];
 }
 
-template <int H>
-__global__ __launch_bounds__(xc::NT, 1) void gru_fwd_xc(FwdArgs a, XcWs ws) {
+template <int H, bool DROP>
+__global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gru_fwd_xc(FwdArgs a, XcWs ws) {
   using C = xc::Cfg<H>;
   constexpr int M = C::M;
   __shared__ __attribute__((aligned(16))) char lds[C::LDS];
@@ -2365,6 +2386,8 @@ __global__ __launch_bounds__(xc::NT, 1) void gru_fwd_xc(FwdArgs a, XcWs ws) {
   char* slots = lds + C::ST;
   float* stg = reinterpret_cast<float*>(lds + C::ST + 2 * C::SLOT);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  uint32_t ho[C::QPW];
+  xc_h_offsets<H>(ho);
   // group / member: blocks b and b + 8 share an XCD under round-robin placement
   const int xcd = blockIdx.x & 7, jj = blockIdx.x >> 3;
   const int grp = xcd * ws.qg + jj / M, mem = jj % M;
@@ -2407,8 +2430,11 @@ __global__ __launch_bounds__(xc::NT, 1) void gru_fwd_xc(FwdArgs a, XcWs ws) {
   bf16_t* Yw = static_cast<bf16_t*>(R.y);
   bf16_t* X1 = static_cast<bf16_t*>(R.x1);
   bf16_t* S = static_cast<bf16_t*>(R.save);
-  const bool drop = X1 && a.drop_thresh;
 
+#ifdef TT_DIAG
+  unsigned long long prf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  TT_STAMP(k_start);
+#endif
   int idx = 0;  // step counter over all rounds: parity of the exchange image, counter target
   for (int r = 0; r < ws.nround; ++r) {
     const int rb0 = gb0 + r * xc::RR;  // first batch row of the round
@@ -2419,72 +2445,85 @@ __global__ __launch_bounds__(xc::NT, 1) void gru_fwd_xc(FwdArgs a, XcWs ws) {
     const __amdgpu_buffer_rsrc_t rY = tt_rsrc_n(Yw + r0w * a.ldy, on);
     const __amdgpu_buffer_rsrc_t rX1 = tt_rsrc_n(X1 ? X1 + r0w * a.ldy : Yw, on && X1 != nullptr);
     const __amdgpu_buffer_rsrc_t rS = tt_rsrc_n(S + r0w * 4L * H, on);
-    for (int i = tid; i < xc::RR * xc::SSTR / 4; i += xc::NT)
-      reinterpret_cast<float4*>(stt)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // a round starts from h_{-1} = 0: zero fp32 state and zero h images, so step 0 runs the
+    // same MFMAs as every other step (0 * W = +0 exactly) and the chunk loop below is one
+    // basic block (the matrix pipe and the gate arithmetic interleave)
+    for (int i = tid; i < (C::ST + 2 * C::SLOT) / 16; i += xc::NT)
+      reinterpret_cast<float4*>(lds)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     // gate inputs of chunk c at step s: 3 x 16 bytes per thread, issued a chunk ahead
+    // (per-lane offset of row cr; the chunk and gate offsets are wave-uniform)
+    const int cstep_g = xc::CR * T_ * (int)a.ldg * 2;
     auto load_g = [&](int s, int c, tt_u32x4 (&gx)[3]) {
       const int t = R.dir ? T_ - 1 - s : s;
-      const int rr = c * xc::CR + cr;
-      const uint32_t og = rr < nrow ? (uint32_t)((rr * T_ + t) * (int)a.ldg + j) * 2u : xc::OOB;
+      const uint32_t og = c * xc::CR + cr < nrow ? (uint32_t)((cr * T_ + t) * (int)a.ldg + j) * 2u : xc::OOB;
 #pragma unroll
-      for (int g = 0; g < 3; ++g) gx[g] = __builtin_amdgcn_raw_buffer_load_b128(rG, (int)og, g * H * 2, 0);
+      for (int g = 0; g < 3; ++g) gx[g] = __builtin_amdgcn_raw_buffer_load_b128(rG, (int)og, c * cstep_g + g * H * 2, 0);
     };
     tt_u32x4 gcur[3], gnxt[3];
     load_g(0, 0, gcur);
     for (int s = 0; s < T_; ++s, ++idx) {
       const int t = R.dir ? T_ - 1 - s : s;
-      const bool mm = s > 0;  // h_{-1} = 0: the first step has no recurrent term
+      const bool mm = s > 0;  // h_{-1} = 0: step 0 reads no exchange image (its slots are zero)
+      TT_STAMP(p0);
       // all members finished step idx-1: its h is complete, and nobody still reads the
       // image this step overwrites (written two steps ago)
-      if (idx > 0 && tid == 0) xc_wait(cnt, (unsigned)(M * idx), err);
+#ifdef TT_DIAG
+      if (!(a.dbg & 1))
+#endif
+        if (idx > 0 && tid == 0) xc_wait(cnt, (unsigned)(M * idx), err);
       __syncthreads();
+      TT_STAMP(p1);
       const __amdgpu_buffer_rsrc_t rsrc_h = rx[(idx - 1) & 1];
       const __amdgpu_buffer_rsrc_t rdst_h = rx[idx & 1];
       tt_u32x4 hv[C::QPW];
       f32x4 acc[2][3];
       if (mm) {
-        xc_load_h<H>(rsrc_h, 0, hv);
+        xc_load_h<H>(rsrc_h, ho, 0, hv);
         xc_put_h<H>(slots, hv);
-        xc_load_h<H>(rsrc_h, 1, hv);
+        xc_load_h<H>(rsrc_h, ho, 1, hv);
       }
       __syncthreads();
+      xc_mfma<H>(slots, wa, acc);
       if (mm) {
-        xc_mfma<H>(slots, wa, acc);
         xc_put_h<H>(slots + C::SLOT, hv);
-        xc_load_h<H>(rsrc_h, 2, hv);
-      } else {
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-          for (int g = 0; g < 3; ++g) acc[rb][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        xc_load_h<H>(rsrc_h, ho, 2, hv);
       }
       xc_stage(stg, acc);
       __syncthreads();
+      // the gates and fp32 state of chunk c into registers, right after its staging barrier:
+      // the arithmetic then depends on registers only and interleaves with the next MFMAs
+      float lr[8], lz[8], ln[8], hp[8];
+      auto read_gates = [&](int c) {
+        const int rr = c * xc::CR + cr;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float4 v0 = *reinterpret_cast<const float4*>(stg + stg_off(cr, 0 * 64 + u0 + 4 * h));
+          const float4 v1 = *reinterpret_cast<const float4*>(stg + stg_off(cr, 1 * 64 + u0 + 4 * h));
+          const float4 v2 = *reinterpret_cast<const float4*>(stg + stg_off(cr, 2 * 64 + u0 + 4 * h));
+          const float4 p = *reinterpret_cast<const float4*>(stt + rr * xc::SSTR + u0 + 4 * h);
+          lr[4 * h] = v0.x; lr[4 * h + 1] = v0.y; lr[4 * h + 2] = v0.z; lr[4 * h + 3] = v0.w;
+          lz[4 * h] = v1.x; lz[4 * h + 1] = v1.y; lz[4 * h + 2] = v1.z; lz[4 * h + 3] = v1.w;
+          ln[4 * h] = v2.x; ln[4 * h + 1] = v2.y; ln[4 * h + 2] = v2.z; ln[4 * h + 3] = v2.w;
+          hp[4 * h] = p.x; hp[4 * h + 1] = p.y; hp[4 * h + 2] = p.z; hp[4 * h + 3] = p.w;
+        }
+      };
+      read_gates(0);
+      TT_STAMP(p2);
 #pragma unroll
       for (int c = 0; c < xc::NCH; ++c) {
+        TT_STAMP(c0);
         if (c + 1 < xc::NCH) {
           load_g(s, c + 1, gnxt);
-          if (mm) xc_mfma<H>(slots + ((c + 1) & 1) * C::SLOT, wa, acc);
+          xc_mfma<H>(slots + ((c + 1) & 1) * C::SLOT, wa, acc);
         }
         // ---- gate arithmetic of chunk c
         {
           const int rr = c * xc::CR + cr;
           const bool ok = rr < nrow;
-          float xr[8], xz[8], xn[8], lr[8], lz[8], ln[8], hp[8], y[8], sr[8], sz[8], sn[8], sg[8];
+          float xr[8], xz[8], xn[8], y[8], sr[8], sz[8], sn[8], sg[8];
           unpack8(make_uint4(gcur[0][0], gcur[0][1], gcur[0][2], gcur[0][3]), xr);
           unpack8(make_uint4(gcur[1][0], gcur[1][1], gcur[1][2], gcur[1][3]), xz);
           unpack8(make_uint4(gcur[2][0], gcur[2][1], gcur[2][2], gcur[2][3]), xn);
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const float4 v0 = *reinterpret_cast<const float4*>(stg + stg_off(cr, 0 * 64 + u0 + 4 * h));
-            const float4 v1 = *reinterpret_cast<const float4*>(stg + stg_off(cr, 1 * 64 + u0 + 4 * h));
-            const float4 v2 = *reinterpret_cast<const float4*>(stg + stg_off(cr, 2 * 64 + u0 + 4 * h));
-            const float4 p = *reinterpret_cast<const float4*>(stt + rr * xc::SSTR + u0 + 4 * h);
-            lr[4 * h] = v0.x; lr[4 * h + 1] = v0.y; lr[4 * h + 2] = v0.z; lr[4 * h + 3] = v0.w;
-            lz[4 * h] = v1.x; lz[4 * h + 1] = v1.y; lz[4 * h + 2] = v1.z; lz[4 * h + 3] = v1.w;
-            ln[4 * h] = v2.x; ln[4 * h + 1] = v2.y; ln[4 * h + 2] = v2.z; ln[4 * h + 3] = v2.w;
-            hp[4 * h] = p.x; hp[4 * h + 1] = p.y; hp[4 * h + 2] = p.z; hp[4 * h + 3] = p.w;
-          }
 #pragma unroll
           for (int e = 0; e < 8; ++e)
             gru_cell(xr[e], xz[e], xn[e], lr[e], lz[e], ln[e], bn[e], hp[e], y[e], sr[e], sz[e], sn[e], sg[e]);
@@ -2493,40 +2532,394 @@ __global__ __launch_bounds__(xc::NT, 1) void gru_fwd_xc(FwdArgs a, XcWs ws) {
           const uint4 yb = pack8bf(y);
           st16_buf_sc1(rdst_h, (uint32_t)(rr * H + j) * 2u, 0, yb);  // the exchange image (all rows)
           const int lrow = rr * T_ + t;
-          const uint32_t oy = ok ? (uint32_t)(lrow * (int)a.ldy + j) * 2u : xc::OOB;
-          const uint32_t os = ok ? (uint32_t)(lrow * 4 * H + j) * 2u : xc::OOB;
+          uint32_t oy = ok ? (uint32_t)(lrow * (int)a.ldy + j) * 2u : xc::OOB;
+          uint32_t os = ok ? (uint32_t)(lrow * 4 * H + j) * 2u : xc::OOB;
+#ifdef TT_DIAG
+          if (a.dbg & 2) oy = os = xc::OOB;  // 2: no Y / S / X1 stores (dropped)
+#endif
           st16_buf(rY, oy, 0, yb);
           st16_buf(rS, os, 0, pack8bf(sr));
           st16_buf(rS, os, 2 * H, pack8bf(sz));
           st16_buf(rS, os, 4 * H, pack8bf(sn));
           st16_buf(rS, os, 6 * H, pack8bf(sg));
-          if (drop) {
+          if constexpr (DROP) {
             const uint32_t grow = (uint32_t)(rb0 + rr) * (uint32_t)T_ + (uint32_t)t;
 #pragma unroll
             for (int e = 0; e < 8; ++e)
               y[e] *= tt_dropout_scale(R.seed, R.row0 + grow, (uint32_t)(R.col0 + j + e), a.drop_thresh, a.inv_keep);
+            st16_buf(rX1, oy, 0, pack8bf(y));
+          } else {
+            st16_buf(rX1, oy, 0, yb);  // dropped unless an eval X1 copy was asked for
           }
-          st16_buf(rX1, oy, 0, pack8bf(y));
+          if (XC_VALU_PER_MFMA > 0 && c + 1 < xc::NCH) {
+            // interleave chunk c+1's MFMAs with this arithmetic: one MFMA, then VALU work
+            // for the matrix pipe's 16 cycles
+            // the first two K-steps' fragment reads, then per K-step six MFMAs, each
+            // followed by VALU work, and the fragment reads two K-steps ahead
+            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+            for (int kt = 0; kt < C::NKT; ++kt) {
+#pragma unroll
+              for (int i = 0; i < 6; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, XC_VALU_PER_MFMA, 0);
+              }
+              if (kt + 2 < C::NKT) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            }
+          }
         }
         if (mm && c + 2 < xc::NCH) {
           xc_put_h<H>(slots + (c & 1) * C::SLOT, hv);  // chunk c+2 into the slot chunk c used
-          if (c + 3 < xc::NCH) xc_load_h<H>(rsrc_h, c + 3, hv);
+          if (c + 3 < xc::NCH) xc_load_h<H>(rsrc_h, ho, c + 3, hv);
         }
+        TT_STAMP(c1);
         __syncthreads();
         if (c + 1 < xc::NCH) {
           xc_stage(stg, acc);
           __syncthreads();
+          read_gates(c + 1);
 #pragma unroll
           for (int g = 0; g < 3; ++g) gcur[g] = gnxt[g];
         }
+        TT_STAMP(c2);
+        TT_ACC(2, c1 - c0);  // chunk: MFMAs + gate arithmetic + h restage issued
+        TT_ACC(3, c2 - c1);  // chunk barriers + gate staging
       }
+      TT_STAMP(p3);
       // publish h_s: every wave drains its stores (the exchange stores are write-through),
       // then one lane counts the workgroup in
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef TT_DIAG
+      if (!(a.dbg & 4))
+#endif
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (s + 1 < T_) load_g(s + 1, 0, gcur);
+      TT_STAMP(p4);
+      TT_ACC(0, p1 - p0);  // wait for the group + barrier
+      TT_ACC(1, p2 - p1);  // prologue: chunks 0-1 of h, MFMAs of chunk 0
+      TT_ACC(4, p4 - p3);  // drain + publish
     }
+  }
+#ifdef TT_DIAG
+  TT_STAMP(k_end);
+  prf[7] = k_end - k_start;
+  if (threadIdx.x == 0 && blockIdx.x < 2048)
+    for (int i = 0; i < 8; ++i) g_fwd_prof[blockIdx.x][i] = prf[i];
+#endif
+}
+
+// ---- column-split persistent backward (gru_bwd_xc, bf16, H 256 / 512) ---------------
+// The BPTT of gru_fwd_xc's split (gru_bwd_rows' per-step math): member m of a group of
+// M = H/64 workgroups owns hidden units [64m, 64m+64) of the group's rows and keeps
+// W_hh[:, its units] (3H x 64, 192 KiB at H 512) in the accumulator registers. Per step
+//   dh_t[rows, own units] = dL/dgh_{t+1}[rows, 3H] . W_hh[3H, own units]
+// needs the gate gradients of ALL units (r | z | W_hn h blocks), so the members exchange
+// those instead: each publishes its 3 x 64 columns of the step's dL/dgh through a group
+// image (16-byte write-through stores, drain, arrival counter) and reads back the 3H
+// columns of every row (write-through loads) -- 3H * 2 bytes per row and step of L2
+// traffic instead of the whole W_hh per 128 rows. The 4 waves split K (3H/4 each, so every
+// operand fragment is read from LDS once per chunk and feeds four MFMAs); the four partial
+// products are summed in a fixed order by the gate arithmetic. Rows run in rounds of 256
+// with the bf16 carry dh*z in LDS, in chunks of 16 rows. Same gate arithmetic and the same
+// bf16 rounding points as gru_bwd_rows (the accumulator, the carry); the K summation order
+// differs (four quarter sums), so results agree with it to bf16 rounding
+// (tests/test_gpu_gru_persistent.py). Bias partials: one row per group (row gi of the
+// recurrence's partial block), written once at the end.
+namespace xb {
+constexpr int NT = 256;
+constexpr int CR = 16;                  // rows per chunk
+constexpr int RR = 256;                 // rows per round
+constexpr int NCH = RR / CR;
+constexpr int PSTG = 4 * CR * 64 * 4;   // four partial products [16 rows][64 units] fp32
+template <int H>
+struct Cfg {
+  static constexpr int M = H / 64;
+  static constexpr int KW = 3 * H / 4;       // K per wave
+  static constexpr int NKS = KW / 32;        // K-steps per wave
+  static constexpr int QPT = 3 * H * CR * 2 / 16 / NT;  // 16-byte exchange loads per thread and chunk
+  static constexpr int SLOT = CR * 3 * H * 2;          // gradient chunk image [K-step][kq][row] x 16 B
+  static constexpr int CARRY = RR * 64 * 2;            // bf16 dh * z of the round's rows
+  static constexpr int LDS = 2 * SLOT + PSTG + CARRY;
+};
+static_assert(Cfg<512>::LDS <= 163840 && Cfg<256>::LDS <= 163840, "gru_bwd_xc LDS budget");
+TT_DEV int pstg_off(int w, int row, int u) {  // 16-byte chunk (u >> 2) of row at (u >> 2) ^ row
+  return ((w * CR + row) * 16 + (((u >> 2) ^ row) & 15)) * 4 + (u & 3);
+}
+}  // namespace xb
+
+struct XbWs {
+  bf16_t* xb;     // [groups][2][RR][3H] exchange images of dL/dgh
+  unsigned* cnt;
+  unsigned* err;
+  int qg, nrec, rpg, nround;
+};
+
+template <int H>
+__global__ __launch_bounds__(xb::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gru_bwd_xc(BwdArgs a, XbWs ws) {
+  using C = xb::Cfg<H>;
+  constexpr int M = C::M, NKS = C::NKS, QPT = C::QPT;
+  __shared__ __attribute__((aligned(16))) char lds[C::LDS];
+  char* slots = lds;
+  float* pst = reinterpret_cast<float*>(lds + 2 * C::SLOT);
+  bf16_t* carry = reinterpret_cast<bf16_t*>(lds + 2 * C::SLOT + xb::PSTG);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int xcd = blockIdx.x & 7, jj = blockIdx.x >> 3;
+  const int grp = xcd * ws.qg + jj / M, mem = jj % M;
+  const int rz = grp % ws.nrec, gi = grp / ws.nrec;
+  const BwdRec R = a.r[rz];
+  const int T_ = a.T, B = a.B;
+  const int gb0 = gi * ws.rpg;
+  xc_gu32* cnt = (xc_gu32*)(uintptr_t)(ws.cnt + grp * xc::CSTR);
+  xc_gu32* err = (xc_gu32*)(uintptr_t)ws.err;
+  bf16_t* xbg = ws.xb + (long)grp * 2 * xb::RR * 3 * H;
+  const __amdgpu_buffer_rsrc_t rx[2] = {tt_rsrc(xbg), tt_rsrc(xbg + xb::RR * 3 * H)};
+
+  // W_hh^T fragments (A operand of the C^T product): wave w covers k in [w KW, (w+1) KW);
+  // K-step ks, unit tile nt: lane holds W_hh[k0 + 8 (lane >> 4) + i][64 mem + 16 nt + (lane & 15)]
+  tt_u32x4 wa[NKS][4];
+  {
+    const bf16_t* W = static_cast<const bf16_t*>(R.whh);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int k0 = wave * C::KW + ks * 32 + (lane >> 4) * 8, u = 64 * mem + 16 * nt + (lane & 15);
+        uint32_t w4[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          w4[i] = (uint32_t)W[(long)(k0 + 2 * i) * H + u] | ((uint32_t)W[(long)(k0 + 2 * i + 1) * H + u] << 16);
+        wa[ks][nt] = tt_u32x4{w4[0], w4[1], w4[2], w4[3]};
+      }
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) asm volatile("" : "+a"(wa[ks][nt]));
+  }
+  // exchange loads: thread piece p of a chunk = 16 bytes (8 k) of one row; the chunk image
+  // is [K-step][kq][row] x 16 B, so the MFMA fragment of K-step kt is 1 KiB contiguous
+  uint32_t xo[QPT], lo[QPT];
+#pragma unroll
+  for (int p = 0; p < QPT; ++p) {
+    const int q = p * xb::NT + tid;             // 16-byte unit of the chunk image
+    const int kt = q >> 6, kq = (q >> 4) & 3, row = q & 15;
+    xo[p] = (uint32_t)((row * 3 * H + kt * 32 + kq * 8) * 2);
+    lo[p] = (uint32_t)(q * 16);
+  }
+  // epilogue ownership: chunk row er, units u0 .. u0+3 of this member's 64
+  const int er = tid >> 4, u0 = (tid & 15) * 4, j = 64 * mem + u0;
+  const bf16_t* S = static_cast<const bf16_t*>(R.save);
+  const bf16_t* Y = static_cast<const bf16_t*>(R.y);
+  const bf16_t* DY = static_cast<const bf16_t*>(R.dy);
+  bf16_t* DGX = static_cast<bf16_t*>(R.dgx);
+  bf16_t* DGH = static_cast<bf16_t*>(R.dgh);
+  float bsum[4][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bsum[q][e] = 0.f;
+
+  int idx = 0;
+  for (int r = 0; r < ws.nround; ++r) {
+    const int rb0 = gb0 + r * xb::RR;
+    const int nrow = min(min(ws.rpg - r * xb::RR, xb::RR), B - rb0);
+    const bool on = nrow > 0;
+    const long r0w = (long)(on ? rb0 : 0) * T_;
+    const __amdgpu_buffer_rsrc_t rS = tt_rsrc_n(S + r0w * 4L * H, on);
+    const __amdgpu_buffer_rsrc_t rY = tt_rsrc_n(Y + r0w * a.ldy, on);
+    const __amdgpu_buffer_rsrc_t rD = tt_rsrc_n(DY ? DY + r0w * a.ldy : Y, on && DY != nullptr);
+    const __amdgpu_buffer_rsrc_t rGX = tt_rsrc_n(DGX + r0w * a.ldd, on);
+    const __amdgpu_buffer_rsrc_t rGH = tt_rsrc_n(DGH + r0w * a.ldd, on);
+    for (int i = tid; i < 2 * C::SLOT / 16; i += xb::NT)
+      reinterpret_cast<float4*>(slots)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // per-chunk inputs of the gate arithmetic: saved r | z | n | gh_n pre-activations, dY,
+    // h_{t-1}: 8 bytes each (4 units), issued a chunk ahead
+    auto load_in = [&](int s, int c, uint2 (&v)[6]) {
+      const int t = R.dir ? T_ - 1 - s : s;
+      const int tp = R.dir ? t + 1 : t - 1;
+      const int rr = c * xb::CR + er;
+      const bool ok = rr < nrow;
+      const uint32_t os = ok ? (uint32_t)((rr * T_ + t) * 4 * H + j) * 2u : xc::OOB;
+      const uint32_t od = ok ? (uint32_t)((rr * T_ + t) * (int)a.ldy + j) * 2u : xc::OOB;
+      const uint32_t oh = ok && s > 0 ? (uint32_t)((rr * T_ + tp) * (int)a.ldy + j) * 2u : xc::OOB;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const auto w = __builtin_amdgcn_raw_buffer_load_b64(rS, (int)os, q * 2 * H, 0);
+        v[q] = make_uint2(w[0], w[1]);
+      }
+      const auto wd = __builtin_amdgcn_raw_buffer_load_b64(rD, (int)od, 0, 0);
+      const auto wh = __builtin_amdgcn_raw_buffer_load_b64(rY, (int)oh, 0, 0);
+      v[4] = make_uint2(wd[0], wd[1]);
+      v[5] = make_uint2(wh[0], wh[1]);
+    };
+    uint2 vcur[6], vnxt[6];
+    load_in(T_ - 1, 0, vcur);
+    for (int s = T_ - 1; s >= 0; --s, ++idx) {
+      const int t = R.dir ? T_ - 1 - s : s;
+      const bool last = s == T_ - 1;  // the first step processed: no recurrent gradient yet
+      const bool mm = !last;
+      if (idx > 0 && tid == 0) xc_wait(cnt, (unsigned)(M * idx), err);
+      __syncthreads();
+      const __amdgpu_buffer_rsrc_t rsrc = rx[(idx - 1) & 1];
+      const __amdgpu_buffer_rsrc_t rdst = rx[idx & 1];
+      tt_u32x4 hv[QPT];
+      auto load_x = [&](int c) {
+#pragma unroll
+        for (int p = 0; p < QPT; ++p)
+          hv[p] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)xo[p], c * xb::CR * 3 * H * 2, 16);
+      };
+      auto put_x = [&](char* slot) {
+#pragma unroll
+        for (int p = 0; p < QPT; ++p) *reinterpret_cast<tt_u32x4*>(slot + lo[p]) = hv[p];
+      };
+      // partial product of chunk c: wave's K quarter x 64 units (C^T: 4 units of a row per lane)
+      f32x4 acc[4];
+      auto mfma = [&](const char* slot) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const char* base = slot + wave * NKS * 1024 + lane * 16;
+        tt_u32x4 f[3];
+        f[0] = *reinterpret_cast<const tt_u32x4*>(base);
+        f[1] = *reinterpret_cast<const tt_u32x4*>(base + 1024);
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          if (ks + 2 < NKS) f[(ks + 2) % 3] = *reinterpret_cast<const tt_u32x4*>(base + (ks + 2) * 1024);
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8v, wa[ks][nt]),
+                                                              __builtin_bit_cast(bf16x8v, f[ks % 3]), acc[nt], 0, 0, 0);
+        }
+      };
+      auto stage = [&]() {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          *reinterpret_cast<f32x4*>(pst + xb::pstg_off(wave, lane & 15, 16 * nt + 4 * (lane >> 4))) = acc[nt];
+      };
+      float gm[4], cin[4];
+      auto read_part = [&](int c) {  // the four K quarters summed in order, rounded like gru_bwd_rows
+        float4 p0 = *reinterpret_cast<const float4*>(pst + xb::pstg_off(0, er, u0));
+        const float4 p1 = *reinterpret_cast<const float4*>(pst + xb::pstg_off(1, er, u0));
+        const float4 p2 = *reinterpret_cast<const float4*>(pst + xb::pstg_off(2, er, u0));
+        const float4 p3 = *reinterpret_cast<const float4*>(pst + xb::pstg_off(3, er, u0));
+        gm[0] = bf2f(f2bf(((p0.x + p1.x) + p2.x) + p3.x));
+        gm[1] = bf2f(f2bf(((p0.y + p1.y) + p2.y) + p3.y));
+        gm[2] = bf2f(f2bf(((p0.z + p1.z) + p2.z) + p3.z));
+        gm[3] = bf2f(f2bf(((p0.w + p1.w) + p2.w) + p3.w));
+        const uint2 cv = *reinterpret_cast<const uint2*>(carry + (c * xb::CR + er) * 64 + u0);
+        cin[0] = __uint_as_float(cv.x << 16); cin[1] = __uint_as_float(cv.x & 0xFFFF0000u);
+        cin[2] = __uint_as_float(cv.y << 16); cin[3] = __uint_as_float(cv.y & 0xFFFF0000u);
+        if (last) {
+          const int b = rb0 + c * xb::CR + er;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) cin[e] = 0.f;
+          if (R.dfinal && c * xb::CR + er < nrow) {
+            const float4 d = *reinterpret_cast<const float4*>(R.dfinal + (long)b * a.ldf + j);
+            cin[0] = d.x; cin[1] = d.y; cin[2] = d.z; cin[3] = d.w;
+          }
+        }
+      };
+      if (mm) {
+        load_x(0);
+        put_x(slots);
+        load_x(1);
+      }
+      __syncthreads();
+      mfma(slots);
+      if (mm) {
+        put_x(slots + C::SLOT);
+        load_x(2);
+      }
+      stage();
+      __syncthreads();
+      read_part(0);
+#pragma unroll
+      for (int c = 0; c < xb::NCH; ++c) {
+        if (c + 1 < xb::NCH) {
+          load_in(s, c + 1, vnxt);
+          mfma(slots + ((c + 1) & 1) * C::SLOT);
+        }
+        {
+          const int rr = c * xb::CR + er;
+          float ar[4], az[4], an[4], gh[4], dy[4], hp[4];
+          auto un4 = [](uint2 v, float (&f)[4]) {
+            f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xFFFF0000u);
+            f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xFFFF0000u);
+          };
+          un4(vcur[0], ar); un4(vcur[1], az); un4(vcur[2], an); un4(vcur[3], gh);
+          un4(vcur[4], dy); un4(vcur[5], hp);
+          float o_r[4], o_z[4], o_n[4], o_hn[4], cout[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float dht = gm[e] + cin[e] + dy[e];
+            float rg, omr, zg, omz, ng, sech2;
+            tt_sigmoid_pair(ar[e], rg, omr);
+            tt_sigmoid_pair(az[e], zg, omz);
+            tt_tanh_sech2(an[e], ng, sech2);
+            const float dnp = dht * omz * sech2;
+            const float drp = dnp * gh[e] * rg * omr;
+            const float dzp = dht * (hp[e] - ng) * zg * omz;
+            o_r[e] = drp; o_z[e] = dzp; o_n[e] = dnp; o_hn[e] = dnp * rg;
+            cout[e] = dht * zg;
+          }
+          auto pk4 = [](const float (&f)[4]) {
+            return make_uint2((uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16),
+                              (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16));
+          };
+          const uint2 br = pk4(o_r), bz = pk4(o_z), bn_ = pk4(o_n), bh = pk4(o_hn);
+          *reinterpret_cast<uint2*>(carry + rr * 64 + u0) = pk4(cout);
+          const bool ok = rr < nrow;
+          if (ok) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              bsum[0][e] += o_r[e]; bsum[1][e] += o_z[e]; bsum[2][e] += o_n[e]; bsum[3][e] += o_hn[e];
+            }
+          }
+          // the exchange image: this member's r | z | W_hn h columns of the row
+          const uint32_t ox = (uint32_t)(rr * 3 * H + j) * 2u;
+          tt_u32x4 w2;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, br), rdst, (int)ox, 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, bz), rdst, (int)(ox + 2u * H), 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, bh), rdst, (int)(ox + 4u * H), 0, 16);
+          (void)w2;
+          const uint32_t og = ok ? (uint32_t)((rr * T_ + t) * (int)a.ldd + j) * 2u : xc::OOB;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, br), rGX, (int)og, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, bz), rGX, (int)(og + 2u * H), 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, bn_), rGX, (int)(og + 4u * H), 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, bh), rGH, (int)og, 0, 0);
+        }
+        if (mm && c + 2 < xb::NCH) {
+          put_x(slots + (c & 1) * C::SLOT);
+          if (c + 3 < xb::NCH) load_x(c + 3);
+        }
+        __syncthreads();
+        if (c + 1 < xb::NCH) {
+          stage();
+          __syncthreads();
+          read_part(c + 1);
+#pragma unroll
+          for (int q = 0; q < 6; ++q) vcur[q] = vnxt[q];
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (s > 0) load_in(s - 1, 0, vcur);
+    }
+  }
+  // bias partials: the 16 threads of a unit quad (one per chunk row) in a fixed order
+  __syncthreads();
+  float* red = pst;  // [16 rows][4 gates][64 units]
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) red[(er * 4 + q) * 64 + u0 + e] = bsum[q][e];
+  __syncthreads();
+  {
+    const int q = tid >> 6, u = tid & 63;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < xb::CR; ++w) v += red[(w * 4 + q) * 64 + u];
+    R.dbias[(long)gi * 4 * H + q * H + 64 * mem + u] = v;
   }
 }
 
@@ -2695,8 +3088,11 @@ static int gru_fwd_xc_launch(const FwdArgs& a, int nrec, int B, int T, int H, lo
   w.cnt = x->cnt;
   w.err = x->cnt + XC_MAX_GROUPS * xc::CSTR;
   TT_CHECK_HIP(hipMemsetAsync(x->cnt, 0, sizeof(unsigned) * ng * xc::CSTR, st));
-  if (H == 512) hipLaunchKernelGGL(gru_fwd_xc<512>, dim3(grid), dim3(xc::NT), 0, st, a, w);
-  else hipLaunchKernelGGL(gru_fwd_xc<256>, dim3(grid), dim3(xc::NT), 0, st, a, w);
+  const bool drop = a.drop_thresh != 0 && a.r[0].x1 != nullptr;
+  if (H == 512 && drop) hipLaunchKernelGGL((gru_fwd_xc<512, true>), dim3(grid), dim3(xc::NT), 0, st, a, w);
+  else if (H == 512) hipLaunchKernelGGL((gru_fwd_xc<512, false>), dim3(grid), dim3(xc::NT), 0, st, a, w);
+  else if (drop) hipLaunchKernelGGL((gru_fwd_xc<256, true>), dim3(grid), dim3(xc::NT), 0, st, a, w);
+  else hipLaunchKernelGGL((gru_fwd_xc<256, false>), dim3(grid), dim3(xc::NT), 0, st, a, w);
   TT_CHECK_LAUNCH("gru_fwd_xc");
   *used = true;
   return 0;

@@ -142,9 +142,12 @@ int tt_gru_fwd_launches(int dtype, int T, int H);
 int tt_gru_fwd_xc_status(int* timed_out);
 
 /* Backward (BPTT) of tt_gru_fwd. Produces dL/dg (= dgx, feeds dWih, dbih and the
- * layer-input gradient) and dL/dgh (feeds dWhh), plus per-tile bias partial sums
- * (one row per 128-row batch tile; columns r|z|n|ghn; reduce with tt_colsum:
- * dbih = [0:3H], dbhh = [0:2H] ++ [3H:4H]). */
+ * layer-input gradient) and dL/dgh (feeds dWhh), plus bias partial sums (one row per
+ * 128-row batch tile, or per row group of the column-split kernel: tt_gru_bias_rows(B) >= 64
+ * rows; columns r|z|n|ghn; reduce with tt_colsum: dbih = [0:3H], dbhh = [0:2H] ++ [3H:4H]).
+ * bf16, H 256 / 512, batch large enough (or option gru_bwd_xc = 2): the column-split
+ * persistent kernel (the BPTT of tt_gru_fwd's: H/64 workgroups exchange the step's gate
+ * gradients through the same per-device workspace; dhstate unused). */
 typedef struct {
   const void* save;    /* [B*T, 4H] from tt_gru_fwd          */
   const void* y;       /* layer output (source of h_{s-1})   */

@@ -20,17 +20,33 @@ NAMES = ["wait + barrier", "prologue (h chunks 0-1, MFMA 0)", "chunk: MFMA + gat
          "chunk: barriers + staging", "drain + publish", "-", "-", "total"]
 
 
+BWD_NAMES = ["wait + barrier", "prologue (chunks 0-1, MFMA 0)", "chunk: MFMA + gates + restage issue",
+             "chunk: barriers + staging + partial sums", "drain + publish", "-", "-", "total"]
+
+
 def main():
     B, T, H = 8192, 64, 512
     dev = torch.device("cuda")
     recs, keep = bench_gru.setup(B, T, H, dev)
     st = stream_ptr(dev)
+    args = sys.argv[1:]
+    bwd = bool(args) and args[0] == "bwd"
+    if bwd:
+        args = args[1:]
+        call("tt_gru_fwd", 1, recs, 4, B, T, H, 6 * H, 2 * H, 0.1, st)
+        brecs, bkeep = bench_gru.setup_bwd(B, T, H, keep, dev)
+        set_option("gru_bwd_xc", 2)
+        global NAMES
+        NAMES = BWD_NAMES
     set_option("gru_fwd_xc", 2)
     lib = _lib.load()
     lib.tt_diag_fwd_prof.restype = ctypes.c_int
-    for dbg in (sys.argv[1:] or ["0"]):
+    for dbg in (args or ["0"]):
         os.environ["TT_GRU_DBG"] = dbg
-        f = lambda: call("tt_gru_fwd", 1, recs, 4, B, T, H, 6 * H, 2 * H, 0.1, st)
+        if bwd:
+            f = lambda: call("tt_gru_bwd", 1, brecs, 4, B, T, H, 2 * H, 8 * H, 2 * H, st)
+        else:
+            f = lambda: call("tt_gru_fwd", 1, recs, 4, B, T, H, 6 * H, 2 * H, 0.1, st)
         f()
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -36,6 +36,7 @@ enum Opt {
   OPT_GEMM_PERSIST_MAXK,  // persistent GEMM for problems of at most this many K-tiles
   OPT_GRU_FWD_PAIR,     // persistent forward: two K-tiles per barrier (4-stage W_hh ring)
   OPT_GRU_FWD_XC,       // column-split persistent forward: 0 off, 1 where the batch fills it, 2 wherever it applies
+  OPT_GRU_BWD_XC,       // column-split persistent backward (experiment, off by default: measured slower): 1 where the batch fills it, 2 wherever it applies
   OPT_N
 };
 int opt(Opt o);

@@ -38,6 +38,7 @@ constexpr OptDef kOpts[OPT_N] = {
     {"gru_fwd_wr", "TT_GRU_FWD_WR", 0},           {"hn_map", "TT_HN_MAP", 0},
     {"gemm_skew", "TT_GEMM_SKEW", 0},             {"gemm_persist_maxk", "TT_GEMM_PERSIST_MAXK", 24},
     {"gru_fwd_pair", "TT_GRU_FWD_PAIR", 0},       {"gru_fwd_xc", "TT_GRU_FWD_XC", 1},
+    {"gru_bwd_xc", "TT_GRU_BWD_XC", 0},
 };
 struct OptTable {
   std::atomic<int> v[OPT_N];

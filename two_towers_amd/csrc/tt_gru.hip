@@ -2265,7 +2265,7 @@ __global__ __launch_bounds__(wr::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
 // 8 * M * (CUs / 8M) <= CUs; every wait is bounded (timeout flag, tt_gru_fwd_xc_status).
 typedef __attribute__((address_space(1))) unsigned xc_gu32;
 #ifndef XC_VALU_PER_MFMA
-#define XC_VALU_PER_MFMA 2
+#define XC_VALU_PER_MFMA 3
 #endif
 namespace xc {
 constexpr int NT = 256;                // 4 waves, one per SIMD
@@ -2296,6 +2296,7 @@ struct XcWs {
   int nrec;       // recurrences (groups are dealt to them round-robin)
   int rpg;        // batch rows per group
   int nround;     // rounds of RR rows per group
+  int fast_ok;    // the exchange may stay in the XCD's L2 where the group shares one
 };
 
 TT_DEV void xc_wait(xc_gu32* cnt, unsigned target, xc_gu32* err) {
@@ -2310,6 +2311,31 @@ TT_DEV void xc_wait(xc_gu32* cnt, unsigned target, xc_gu32* err) {
     }
     __builtin_amdgcn_s_sleep(1);
   }
+}
+
+// Whether every member of a group runs on one XCD (HW_REG_XCC_ID), decided identically by
+// all members at launch start: then the exchange images may be written with plain stores,
+// which keep the lines in that XCD's L2 (the members' write-through loads bypass only their
+// own L1, so they read the L2 copy); otherwise every image store is write-through (sc1) and
+// the readers fetch from the Infinity Cache. Placement changes only the speed, never the
+// result. Counter words: [0] step arrivals, [1] start arrivals, [8 + m] member m's XCD + 1.
+TT_DEV bool xc_group_on_one_xcd(unsigned* cntw, int M, int mem, bool allowed, xc_gu32* err) {
+  __shared__ int s_fast;
+  if (threadIdx.x == 0) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xc_gu32* w = (xc_gu32*)(uintptr_t)cntw;
+    __hip_atomic_store(w + 8 + mem, (xcc & 15u) + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(w + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    xc_wait(w + 1, (unsigned)M, err);
+    unsigned first = __hip_atomic_load(w + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool same = allowed && first != 0u;
+    for (int m = 1; m < M; ++m) same &= __hip_atomic_load(w + 8 + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == first;
+    s_fast = same ? 1 : 0;
+  }
+  __syncthreads();
+  return s_fast != 0;
 }
 
 // h rows [32c, 32c+32) of an exchange image -> registers (write-through loads): piece p of
@@ -2431,6 +2457,7 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
   bf16_t* X1 = static_cast<bf16_t*>(R.x1);
   bf16_t* S = static_cast<bf16_t*>(R.save);
 
+  const bool fast = xc_group_on_one_xcd(ws.cnt + grp * xc::CSTR, M, mem, ws.fast_ok != 0, err);
 #ifdef TT_DIAG
   unsigned long long prf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   TT_STAMP(k_start);
@@ -2459,11 +2486,17 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
 #pragma unroll
       for (int g = 0; g < 3; ++g) gx[g] = __builtin_amdgcn_raw_buffer_load_b128(rG, (int)og, c * cstep_g + g * H * 2, 0);
     };
-    tt_u32x4 gcur[3], gnxt[3];
-    load_g(0, 0, gcur);
+    // a ring of three gate-input sets: chunk c's in gq[c % 3], requested two chunks ahead
+    tt_u32x4 gq[3][3];
+    load_g(0, 0, gq[0]);
+    load_g(0, 1, gq[1]);
     for (int s = 0; s < T_; ++s, ++idx) {
       const int t = R.dir ? T_ - 1 - s : s;
+#ifdef TT_DIAG
+      const bool mm = s > 0 && !(a.dbg & 8);  // 8: no exchange loads (timing only)
+#else
       const bool mm = s > 0;  // h_{-1} = 0: step 0 reads no exchange image (its slots are zero)
+#endif
       TT_STAMP(p0);
       // all members finished step idx-1: its h is complete, and nobody still reads the
       // image this step overwrites (written two steps ago)
@@ -2512,25 +2545,72 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
 #pragma unroll
       for (int c = 0; c < xc::NCH; ++c) {
         TT_STAMP(c0);
-        if (c + 1 < xc::NCH) {
-          load_g(s, c + 1, gnxt);
-          xc_mfma<H>(slots + ((c + 1) & 1) * C::SLOT, wa, acc);
-        }
-        // ---- gate arithmetic of chunk c
+        if (c + 2 < xc::NCH) load_g(s, c + 2, gq[(c + 2) % 3]);
+        // ---- gate arithmetic of chunk c, woven into the MFMAs of chunk c+1: one K-step
+        // (six MFMAs) and a share of the cells per scheduling region, so the matrix pipe
+        // and the VALU run side by side in each wave (one wave per SIMD)
         {
           const int rr = c * xc::CR + cr;
           const bool ok = rr < nrow;
           float xr[8], xz[8], xn[8], y[8], sr[8], sz[8], sn[8], sg[8];
+          const tt_u32x4(&gcur)[3] = gq[c % 3];
           unpack8(make_uint4(gcur[0][0], gcur[0][1], gcur[0][2], gcur[0][3]), xr);
           unpack8(make_uint4(gcur[1][0], gcur[1][1], gcur[1][2], gcur[1][3]), xz);
           unpack8(make_uint4(gcur[2][0], gcur[2][1], gcur[2][2], gcur[2][3]), xn);
+          if (c + 1 < xc::NCH) {
+            constexpr int NKT = C::NKT;
+            const char* base = slots + ((c + 1) & 1) * C::SLOT + lane * 16;
+            auto frag = [&](int kt, int rb) { return *reinterpret_cast<const tt_u32x4*>(base + (kt * 2 + rb) * 1024); };
 #pragma unroll
-          for (int e = 0; e < 8; ++e)
-            gru_cell(xr[e], xz[e], xn[e], lr[e], lz[e], ln[e], bn[e], hp[e], y[e], sr[e], sz[e], sn[e], sg[e]);
+            for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+              for (int g = 0; g < 3; ++g) acc[rb][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+            tt_u32x4 f[3][2];
+            f[0][0] = frag(0, 0); f[0][1] = frag(0, 1);
+            f[1][0] = frag(1, 0); f[1][1] = frag(1, 1);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int kt = 0; kt < NKT; ++kt) {
+              if (kt + 2 < NKT) {
+                f[(kt + 2) % 3][0] = frag(kt + 2, 0);
+                f[(kt + 2) % 3][1] = frag(kt + 2, 1);
+              }
+#pragma unroll
+              for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+                for (int g = 0; g < 3; ++g)
+                  acc[rb][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                      __builtin_bit_cast(bf16x8v, wa[g][kt]), __builtin_bit_cast(bf16x8v, f[kt % 3][rb]), acc[rb][g], 0, 0, 0);
+#pragma unroll
+              for (int e = 0; e < 8; ++e)
+                if ((e + 1) * NKT / 8 - 1 == kt) {
+                  // opaque inputs and outputs pin the cell to this K-step's region
+                  asm volatile("" : "+v"(xr[e]), "+v"(xz[e]), "+v"(xn[e]), "+v"(lr[e]), "+v"(lz[e]), "+v"(ln[e]),
+                               "+v"(hp[e]));
+                  gru_cell(xr[e], xz[e], xn[e], lr[e], lz[e], ln[e], bn[e], hp[e], y[e], sr[e], sz[e], sn[e], sg[e]);
+                  asm volatile("" : "+v"(y[e]), "+v"(sr[e]), "+v"(sz[e]), "+v"(sn[e]), "+v"(sg[e]));
+                }
+#pragma unroll
+              for (int i = 0; i < 6; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, XC_VALU_PER_MFMA, 0);
+              }
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              gru_cell(xr[e], xz[e], xn[e], lr[e], lz[e], ln[e], bn[e], hp[e], y[e], sr[e], sz[e], sn[e], sg[e]);
+          }
           *reinterpret_cast<float4*>(stt + rr * xc::SSTR + u0) = make_float4(y[0], y[1], y[2], y[3]);
           *reinterpret_cast<float4*>(stt + rr * xc::SSTR + u0 + 4) = make_float4(y[4], y[5], y[6], y[7]);
           const uint4 yb = pack8bf(y);
-          st16_buf_sc1(rdst_h, (uint32_t)(rr * H + j) * 2u, 0, yb);  // the exchange image (all rows)
+          // the exchange image (all rows): L2-resident where the group shares an XCD
+          if (fast) st16_buf(rdst_h, (uint32_t)(rr * H + j) * 2u, 0, yb);
+          else st16_buf_sc1(rdst_h, (uint32_t)(rr * H + j) * 2u, 0, yb);
+          // exactly 6 stores follow (Y, S r/z/n/gh_n, X1): the publish waits
+          // for the exchange store only, not for them
+          asm volatile("" ::: "memory");
           const int lrow = rr * T_ + t;
           uint32_t oy = ok ? (uint32_t)(lrow * (int)a.ldy + j) * 2u : xc::OOB;
           uint32_t os = ok ? (uint32_t)(lrow * 4 * H + j) * 2u : xc::OOB;
@@ -2551,22 +2631,6 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
           } else {
             st16_buf(rX1, oy, 0, yb);  // dropped unless an eval X1 copy was asked for
           }
-          if (XC_VALU_PER_MFMA > 0 && c + 1 < xc::NCH) {
-            // interleave chunk c+1's MFMAs with this arithmetic: one MFMA, then VALU work
-            // for the matrix pipe's 16 cycles
-            // the first two K-steps' fragment reads, then per K-step six MFMAs, each
-            // followed by VALU work, and the fragment reads two K-steps ahead
-            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-            for (int kt = 0; kt < C::NKT; ++kt) {
-#pragma unroll
-              for (int i = 0; i < 6; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, XC_VALU_PER_MFMA, 0);
-              }
-              if (kt + 2 < C::NKT) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-            }
-          }
         }
         if (mm && c + 2 < xc::NCH) {
           xc_put_h<H>(slots + (c & 1) * C::SLOT, hv);  // chunk c+2 into the slot chunk c used
@@ -2578,8 +2642,6 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
           xc_stage(stg, acc);
           __syncthreads();
           read_gates(c + 1);
-#pragma unroll
-          for (int g = 0; g < 3; ++g) gcur[g] = gnxt[g];
         }
         TT_STAMP(c2);
         TT_ACC(2, c1 - c0);  // chunk: MFMAs + gate arithmetic + h restage issued
@@ -2591,10 +2653,13 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
 #ifdef TT_DIAG
       if (!(a.dbg & 4))
 #endif
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // all but the last chunk's 6 output stores
       __syncthreads();
       if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (s + 1 < T_) load_g(s + 1, 0, gcur);
+      if (s + 1 < T_) {
+        load_g(s + 1, 0, gq[0]);
+        load_g(s + 1, 1, gq[1]);
+      }
       TT_STAMP(p4);
       TT_ACC(0, p1 - p0);  // wait for the group + barrier
       TT_ACC(1, p2 - p1);  // prologue: chunks 0-1 of h, MFMAs of chunk 0
@@ -2698,14 +2763,10 @@ __global__ __launch_bounds__(xb::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
   }
   // exchange loads: thread piece p of a chunk = 16 bytes (8 k) of one row; the chunk image
   // is [K-step][kq][row] x 16 B, so the MFMA fragment of K-step kt is 1 KiB contiguous
-  uint32_t xo[QPT], lo[QPT];
-#pragma unroll
-  for (int p = 0; p < QPT; ++p) {
-    const int q = p * xb::NT + tid;             // 16-byte unit of the chunk image
-    const int kt = q >> 6, kq = (q >> 4) & 3, row = q & 15;
-    xo[p] = (uint32_t)((row * 3 * H + kt * 32 + kq * 8) * 2);
-    lo[p] = (uint32_t)(q * 16);
-  }
+  // (16-byte unit q = p * 256 + tid of the image: K-step q >> 6, kq (q >> 4) & 3, row q & 15,
+  // so piece p is 256 bytes further along the exchange row and 4 KiB further in LDS)
+  const uint32_t xo0 = (uint32_t)(((tid & 15) * 3 * H + (tid >> 6) * 32 + ((tid >> 4) & 3) * 8) * 2);
+  const uint32_t lo0 = (uint32_t)(tid * 16);
   // epilogue ownership: chunk row er, units u0 .. u0+3 of this member's 64
   const int er = tid >> 4, u0 = (tid & 15) * 4, j = 64 * mem + u0;
   const bf16_t* S = static_cast<const bf16_t*>(R.save);
@@ -2719,6 +2780,13 @@ __global__ __launch_bounds__(xb::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
 #pragma unroll
     for (int e = 0; e < 4; ++e) bsum[q][e] = 0.f;
 
+#ifdef TT_DIAG
+  unsigned long long prf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  TT_STAMP(k_start);
+  const int dbg = a.dbg;  // 1 no group wait, 2 no output stores, 4 no drain, 8 no MFMA, 16 no exchange loads
+#else
+  constexpr int dbg = 0;
+#endif
   int idx = 0;
   for (int r = 0; r < ws.nround; ++r) {
     const int rb0 = gb0 + r * xb::RR;
@@ -2757,26 +2825,29 @@ __global__ __launch_bounds__(xb::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
     for (int s = T_ - 1; s >= 0; --s, ++idx) {
       const int t = R.dir ? T_ - 1 - s : s;
       const bool last = s == T_ - 1;  // the first step processed: no recurrent gradient yet
-      const bool mm = !last;
-      if (idx > 0 && tid == 0) xc_wait(cnt, (unsigned)(M * idx), err);
+      const bool mm = !last && !(dbg & 16);
+      TT_STAMP(p0);
+      if (idx > 0 && tid == 0 && !(dbg & 1)) xc_wait(cnt, (unsigned)(M * idx), err);
       __syncthreads();
+      TT_STAMP(p1);
       const __amdgpu_buffer_rsrc_t rsrc = rx[(idx - 1) & 1];
       const __amdgpu_buffer_rsrc_t rdst = rx[idx & 1];
       tt_u32x4 hv[QPT];
       auto load_x = [&](int c) {
 #pragma unroll
         for (int p = 0; p < QPT; ++p)
-          hv[p] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)xo[p], c * xb::CR * 3 * H * 2, 16);
+          hv[p] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(xo0 + p * 256), c * xb::CR * 3 * H * 2, 16);
       };
       auto put_x = [&](char* slot) {
 #pragma unroll
-        for (int p = 0; p < QPT; ++p) *reinterpret_cast<tt_u32x4*>(slot + lo[p]) = hv[p];
+        for (int p = 0; p < QPT; ++p) *reinterpret_cast<tt_u32x4*>(slot + lo0 + p * 4096) = hv[p];
       };
       // partial product of chunk c: wave's K quarter x 64 units (C^T: 4 units of a row per lane)
       f32x4 acc[4];
       auto mfma = [&](const char* slot) {
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (dbg & 8) return;
         const char* base = slot + wave * NKS * 1024 + lane * 16;
         tt_u32x4 f[3];
         f[0] = *reinterpret_cast<const tt_u32x4*>(base);
@@ -2832,8 +2903,10 @@ __global__ __launch_bounds__(xb::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
       stage();
       __syncthreads();
       read_part(0);
-#pragma unroll
+      TT_STAMP(p2);
+#pragma unroll 1
       for (int c = 0; c < xb::NCH; ++c) {
+        TT_STAMP(c0);
         if (c + 1 < xb::NCH) {
           load_in(s, c + 1, vnxt);
           mfma(slots + ((c + 1) & 1) * C::SLOT);
@@ -2881,7 +2954,7 @@ __global__ __launch_bounds__(xb::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, bz), rdst, (int)(ox + 2u * H), 0, 16);
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, bh), rdst, (int)(ox + 4u * H), 0, 16);
           (void)w2;
-          const uint32_t og = ok ? (uint32_t)((rr * T_ + t) * (int)a.ldd + j) * 2u : xc::OOB;
+          const uint32_t og = ok && !(dbg & 2) ? (uint32_t)((rr * T_ + t) * (int)a.ldd + j) * 2u : xc::OOB;
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, br), rGX, (int)og, 0, 0);
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, bz), rGX, (int)(og + 2u * H), 0, 0);
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, bn_), rGX, (int)(og + 4u * H), 0, 16);
@@ -2891,6 +2964,7 @@ __global__ __launch_bounds__(xb::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
           put_x(slots + (c & 1) * C::SLOT);
           if (c + 3 < xb::NCH) load_x(c + 3);
         }
+        TT_STAMP(c1);
         __syncthreads();
         if (c + 1 < xb::NCH) {
           stage();
@@ -2899,11 +2973,19 @@ __global__ __launch_bounds__(xb::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
 #pragma unroll
           for (int q = 0; q < 6; ++q) vcur[q] = vnxt[q];
         }
+        TT_STAMP(c2);
+        TT_ACC(2, c1 - c0);
+        TT_ACC(3, c2 - c1);
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      TT_STAMP(p3);
+      if (!(dbg & 4)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (s > 0) load_in(s - 1, 0, vcur);
+      TT_STAMP(p4);
+      TT_ACC(0, p1 - p0);
+      TT_ACC(1, p2 - p1);
+      TT_ACC(4, p4 - p3);
     }
   }
   // bias partials: the 16 threads of a unit quad (one per chunk row) in a fixed order
@@ -2921,6 +3003,12 @@ __global__ __launch_bounds__(xb::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
     for (int w = 0; w < xb::CR; ++w) v += red[(w * 4 + q) * 64 + u];
     R.dbias[(long)gi * 4 * H + q * H + 64 * mem + u] = v;
   }
+#ifdef TT_DIAG
+  TT_STAMP(k_end);
+  prf[7] = k_end - k_start;
+  if (threadIdx.x == 0 && blockIdx.x < 2048)
+    for (int i = 0; i < 8; ++i) g_fwd_prof[blockIdx.x][i] = prf[i];
+#endif
 }
 
 #ifdef TT_DIAG
@@ -2958,7 +3046,8 @@ static int bwd_rows() { return tt::opt(tt::OPT_GRU_BWD_ROWS) == 64 ? 64 : 128; }
 // partial bias rows: one per backward row tile (64 rows with gru_bwd_r64; extra rows of
 // a smaller-tile count are zero-filled by tt_gru_bwd and add nothing)
 extern "C" int tt_gru_bias_rows(int B) {
-  return tt_ceil_div(B, tt::opt(tt::OPT_GRU_BWD_R64) ? 64 : bwd_rows());
+  // at least 64: the column-split backward writes one row per group of its recurrence
+  return std::max(64, tt_ceil_div(B, tt::opt(tt::OPT_GRU_BWD_R64) ? 64 : bwd_rows()));
 }
 
 extern "C" int tt_gru_fwd_launches(int dtype, int T, int H) { return gru_fwd_persistent(dtype, H) ? 1 : T; }
@@ -3004,6 +3093,8 @@ struct XcDev {
   size_t xb_bytes = 0;
   bf16_t* xb = nullptr;
   unsigned* cnt = nullptr;  // [512 groups][CSTR] + the timeout flag after them
+  size_t xg_bytes = 0;
+  bf16_t* xg = nullptr;     // gru_bwd_xc exchange images
 };
 static std::mutex g_xc_mu;
 static XcDev g_xc[64];
@@ -3022,13 +3113,14 @@ static bool xc_geometry(int dtype, int H, int nrec, int B, int T, long ldg, long
   if (qg < 1 || ng > XC_MAX_GROUPS || ng % nrec != 0) return false;
   const int gpr = ng / nrec;
   // auto mode: only where every group gets at least half a round of rows
-  if (v == 1 && (long)B < (long)gpr * (xc::RR / 2)) return false;
+  if ((v & 3) == 1 && (long)B < (long)gpr * (xc::RR / 2)) return false;
   // per-round resources: byte offsets of RR rows x T steps stay below 2 GiB
   if ((long)xc::RR * T * std::max({4L * H, ldy, ldg}) * 2 >= (1L << 31)) return false;
   w.qg = qg;
   w.nrec = nrec;
   w.rpg = tt_ceil_div(B, gpr);
   w.nround = tt_ceil_div(w.rpg, xc::RR);
+  w.fast_ok = (v & 4) ? 0 : 1;  // option bit 4: always write-through images
   grid = ng * M;
   return true;
 }
@@ -3094,6 +3186,61 @@ static int gru_fwd_xc_launch(const FwdArgs& a, int nrec, int B, int T, int H, lo
   else if (drop) hipLaunchKernelGGL((gru_fwd_xc<256, true>), dim3(grid), dim3(xc::NT), 0, st, a, w);
   else hipLaunchKernelGGL((gru_fwd_xc<256, false>), dim3(grid), dim3(xc::NT), 0, st, a, w);
   TT_CHECK_LAUNCH("gru_fwd_xc");
+  *used = true;
+  return 0;
+}
+
+// Launch geometry of the column-split backward, or false where it does not apply (bias
+// partial rows: one per group, so the recurrence's partial block must have that many).
+static bool xb_geometry(int H, int nrec, int B, int T, long ldy, long ldd, int cus, XbWs& w, int& grid) {
+  const int v = tt::opt(tt::OPT_GRU_BWD_XC);
+  if (v == 0 || (H != 512 && H != 256) || tt::opt(tt::OPT_GRU_BWD_PERSIST) == 0 || tt::opt(tt::OPT_GRU_BWD_R64) ||
+      bwd_rows() != 128)
+    return false;
+  const int M = H / 64;
+  const int qg = cus / (8 * M);
+  const int ng = 8 * qg;
+  if (qg < 1 || ng > XC_MAX_GROUPS || ng % nrec != 0) return false;
+  const int gpr = ng / nrec;
+  if (tt_gru_bias_rows(B) < gpr) return false;
+  if (v == 1 && (long)B < (long)gpr * (xb::RR / 2)) return false;
+  if ((long)xb::RR * T * std::max({4L * H, ldy, ldd}) * 2 >= (1L << 31)) return false;
+  w.qg = qg;
+  w.nrec = nrec;
+  w.rpg = tt_ceil_div(B, gpr);
+  w.nround = tt_ceil_div(w.rpg, xb::RR);
+  grid = ng * M;
+  return true;
+}
+
+static int gru_bwd_xc_launch(const BwdArgs& a, int nrec, int B, int T, int H, long ldy, long ldd, hipStream_t st,
+                             bool* used) {
+  *used = false;
+  if (tt::opt(tt::OPT_GRU_BWD_XC) == 0 || (H != 512 && H != 256)) return 0;
+  XcDev* x = nullptr;
+  TT_PROPAGATE(xc_device(&x));
+  XbWs w{};
+  int grid = 0;
+  if (!xb_geometry(H, nrec, B, T, ldy, ldd, x->cus, w, grid)) return 0;
+  const int ng = grid / (H / 64);
+  {
+    std::lock_guard<std::mutex> lock(g_xc_mu);
+    const size_t need = (size_t)ng * 2 * xb::RR * 3 * H * sizeof(bf16_t);
+    if (x->xg_bytes < need) {
+      if (x->xg) TT_CHECK_HIP(hipFree(x->xg));
+      x->xg = nullptr;
+      x->xg_bytes = 0;
+      TT_CHECK_HIP(hipMalloc(reinterpret_cast<void**>(&x->xg), need));
+      x->xg_bytes = need;
+    }
+  }
+  w.xb = x->xg;
+  w.cnt = x->cnt;
+  w.err = x->cnt + XC_MAX_GROUPS * xc::CSTR;
+  TT_CHECK_HIP(hipMemsetAsync(x->cnt, 0, sizeof(unsigned) * ng * xc::CSTR, st));
+  if (H == 512) hipLaunchKernelGGL(gru_bwd_xc<512>, dim3(grid), dim3(xb::NT), 0, st, a, w);
+  else hipLaunchKernelGGL(gru_bwd_xc<256>, dim3(grid), dim3(xb::NT), 0, st, a, w);
+  TT_CHECK_LAUNCH("gru_bwd_xc");
   *used = true;
   return 0;
 }
@@ -3231,6 +3378,9 @@ extern "C" int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B
   // bf16, H 256 / 512: one row-owning launch per layer (option gru_bwd_persist = 0: per-step
   // launches)
   if (gru_bwd_persistent(dtype, H)) {
+    bool used = false;
+    TT_PROPAGATE(gru_bwd_xc_launch(a, nrec, B, T, H, ldy, ldd, st, &used));
+    if (used) return 0;
     TT_CHECK_ARG(128L * T * std::max({ldd, ldy, 4L * H}) * esz < (1L << 31), "tt_gru_bwd: tile offsets exceed 2 GiB");
     if (tt::opt(tt::OPT_GRU_BWD_R64)) {
       const dim3 grid(tt_ceil_div(B, 64) * nrec);

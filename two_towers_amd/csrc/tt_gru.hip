@@ -2552,7 +2552,8 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
         {
           const int rr = c * xc::CR + cr;
           const bool ok = rr < nrow;
-          float xr[8], xz[8], xn[8], y[8], sr[8], sz[8], sn[8], sg[8];
+          float xr[8], xz[8], xn[8], y[8], sr[8], sz[8], sn[8], sg[8], msk[8];
+          const uint32_t grow = (uint32_t)(rb0 + rr) * (uint32_t)T_ + (uint32_t)t;
           const tt_u32x4(&gcur)[3] = gq[c % 3];
           unpack8(make_uint4(gcur[0][0], gcur[0][1], gcur[0][2], gcur[0][3]), xr);
           unpack8(make_uint4(gcur[1][0], gcur[1][1], gcur[1][2], gcur[1][3]), xz);
@@ -2581,6 +2582,14 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
                 for (int g = 0; g < 3; ++g)
                   acc[rb][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                       __builtin_bit_cast(bf16x8v, wa[g][kt]), __builtin_bit_cast(bf16x8v, f[kt % 3][rb]), acc[rb][g], 0, 0, 0);
+              if constexpr (DROP) {  // the dropout mask of element e (independent of the cell)
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                  if (e * NKT / 8 == kt) {
+                    msk[e] = tt_dropout_scale(R.seed, R.row0 + grow, (uint32_t)(R.col0 + j + e), a.drop_thresh, a.inv_keep);
+                    asm volatile("" : "+v"(msk[e]));
+                  }
+              }
 #pragma unroll
               for (int e = 0; e < 8; ++e)
                 if ((e + 1) * NKT / 8 - 1 == kt) {
@@ -2599,8 +2608,11 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
             }
           } else {
 #pragma unroll
-            for (int e = 0; e < 8; ++e)
+            for (int e = 0; e < 8; ++e) {
               gru_cell(xr[e], xz[e], xn[e], lr[e], lz[e], ln[e], bn[e], hp[e], y[e], sr[e], sz[e], sn[e], sg[e]);
+              if constexpr (DROP)
+                msk[e] = tt_dropout_scale(R.seed, R.row0 + grow, (uint32_t)(R.col0 + j + e), a.drop_thresh, a.inv_keep);
+            }
           }
           *reinterpret_cast<float4*>(stt + rr * xc::SSTR + u0) = make_float4(y[0], y[1], y[2], y[3]);
           *reinterpret_cast<float4*>(stt + rr * xc::SSTR + u0 + 4) = make_float4(y[4], y[5], y[6], y[7]);
@@ -2623,10 +2635,8 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
           st16_buf(rS, os, 4 * H, pack8bf(sn));
           st16_buf(rS, os, 6 * H, pack8bf(sg));
           if constexpr (DROP) {
-            const uint32_t grow = (uint32_t)(rb0 + rr) * (uint32_t)T_ + (uint32_t)t;
 #pragma unroll
-            for (int e = 0; e < 8; ++e)
-              y[e] *= tt_dropout_scale(R.seed, R.row0 + grow, (uint32_t)(R.col0 + j + e), a.drop_thresh, a.inv_keep);
+            for (int e = 0; e < 8; ++e) y[e] *= msk[e];
             st16_buf(rX1, oy, 0, pack8bf(y));
           } else {
             st16_buf(rX1, oy, 0, yb);  // dropped unless an eval X1 copy was asked for

@@ -237,6 +237,11 @@ def main():
             tdist.init_process_group(backend)
     import two_towers_amd as tta
     from two_towers_amd import dist as tdp
+    if backend != "nccl" and world > max(torch.cuda.device_count(), 1):
+        # ranks sharing one GPU (gloo rehearsal): the column-split GRU kernels need every
+        # CU of the device for one launch, so two ranks' launches would only time out
+        tta._lib.set_option("gru_fwd_xc", 0)
+        tta._lib.set_option("gru_bwd_xc", 0)
     from two_towers_amd import timing
 
     if args.gpus != world:

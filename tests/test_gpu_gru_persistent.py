@@ -153,8 +153,9 @@ def test_column_split_forward_matches_per_step(H, B, T, ntow):
     G, whh, bhn = _inputs(ntow, B, T, H, seed=11 * H + B + T + ntow)
     outs_s = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=1)
     # 2: images kept in the XCD's L2 where a group shares one (the usual placement);
-    # 6: every image store write-through, as for a group split over XCDs
-    for mode in (2, 6):
+    # 6: every image store write-through, as for a group split over XCDs; 10: the form
+    # that waits for the whole previous step (gru_fwd_xc) instead of half steps (gru_fwd_xcp)
+    for mode in (2, 6, 10):
         with option("gru_fwd_xc", mode):
             outs_p = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=0)
         assert _xc_timed_out() == 0

@@ -136,7 +136,7 @@ def main():
         set_option("gru_fwd_pair", {"pair": 1, "ew": 2, "ds": 3, "ds2": 4, "tm": 5, "s16": 6}.get(kind, 0))
         os.environ["TT_GRU_DBG"] = dbg  # read only by a -DTT_DIAG build
         set_option("gru_depth", int(depth[0]) if depth else 4)
-        set_option("gru_fwd_xc", {"xc": 2, "xcs": 6}.get(kind, 0))
+        set_option("gru_fwd_xc", {"xc": 2, "xcs": 6, "xco": 10}.get(kind, 0))
         f = lambda: call("tt_gru_fwd", 1, recs, 4, a.B, a.T, a.H, 6 * a.H, 2 * a.H, 0.1, st)
         f()
         torch.cuda.synchronize()

@@ -2684,6 +2684,257 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
 #endif
 }
 
+// gru_fwd_xcp: gru_fwd_xc with the step boundary pipelined away. The chunks of all steps
+// form one stream: the h chunks three ahead are requested across the step boundary, the
+// MFMAs of the next step's first chunk are woven into this step's last gate arithmetic, and
+// the members publish each half step (chunks 0-3, 4-7) on its own counter, so a member
+// waits for the first half of step s only while it computes the second half of step s-1
+// of its own. Same arithmetic, same order, same outputs as gru_fwd_xc (bit-identical).
+template <int H, bool DROP>
+__global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gru_fwd_xcp(FwdArgs a, XcWs ws) {
+  using C = xc::Cfg<H>;
+  constexpr int M = C::M, NKT = C::NKT;
+  __shared__ __attribute__((aligned(16))) char lds[C::LDS];
+  float* stt = reinterpret_cast<float*>(lds);
+  char* slots = lds + C::ST;
+  float* stg = reinterpret_cast<float*>(lds + C::ST + 2 * C::SLOT);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  uint32_t ho[C::QPW];
+  xc_h_offsets<H>(ho);
+  const int xcd = blockIdx.x & 7, jj = blockIdx.x >> 3;
+  const int grp = xcd * ws.qg + jj / M, mem = jj % M;
+  const int rz = grp % ws.nrec, gi = grp / ws.nrec;
+  const FwdRec R = a.r[rz];
+  const int T_ = a.T, B = a.B;
+  const int gb0 = gi * ws.rpg;
+  xc_gu32* cw = (xc_gu32*)(uintptr_t)(ws.cnt + grp * xc::CSTR);
+  xc_gu32* cntA = cw;      // arrivals of half steps A (chunks 0-3)
+  xc_gu32* cntB = cw + 2;  // and B (chunks 4-7)
+  xc_gu32* err = (xc_gu32*)(uintptr_t)ws.err;
+  bf16_t* xbg = ws.xb + (long)grp * 2 * xc::RR * H;
+  const __amdgpu_buffer_rsrc_t rx[2] = {tt_rsrc(xbg), tt_rsrc(xbg + xc::RR * H)};
+  tt_u32x4 wa[3][NKT];
+  {
+    const bf16_t* W = static_cast<const bf16_t*>(R.whh);
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt)
+        wa[g][kt] = *reinterpret_cast<const tt_u32x4*>(
+            W + (long)(g * H + 64 * mem + 16 * wave + (lane & 15)) * H + kt * 32 + (lane >> 4) * 8);
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) asm volatile("" : "+a"(wa[g][kt]));
+  }
+  const int cr = tid >> 3, u0 = (tid & 7) * 8, j = 64 * mem + u0;
+  float bn[8];
+  {
+    const float4 b0 = *reinterpret_cast<const float4*>(R.bhn + j);
+    const float4 b1 = *reinterpret_cast<const float4*>(R.bhn + j + 4);
+    bn[0] = b0.x; bn[1] = b0.y; bn[2] = b0.z; bn[3] = b0.w;
+    bn[4] = b1.x; bn[5] = b1.y; bn[6] = b1.z; bn[7] = b1.w;
+  }
+  const bf16_t* G = static_cast<const bf16_t*>(R.g);
+  bf16_t* Yw = static_cast<bf16_t*>(R.y);
+  bf16_t* X1 = static_cast<bf16_t*>(R.x1);
+  bf16_t* S = static_cast<bf16_t*>(R.save);
+  const bool fast = xc_group_on_one_xcd(ws.cnt + grp * xc::CSTR, M, mem, ws.fast_ok != 0, err);
+  const int NS = ws.nround * T_;  // steps over all rounds
+  // step idx -> its step in the round, time, first batch row, rows
+  struct Step {
+    int s, t, rb0, nrow;
+  };
+  auto step_of = [&](int idx) {
+    Step q;
+    const int r = idx / T_;
+    q.s = idx - r * T_;
+    q.t = R.dir ? T_ - 1 - q.s : q.s;
+    q.rb0 = gb0 + r * xc::RR;
+    q.nrow = min(min(ws.rpg - r * xc::RR, xc::RR), B - q.rb0);
+    return q;
+  };
+  auto g_rsrc = [&](const Step& q) {
+    return tt_rsrc_n(G + (long)(q.nrow > 0 ? q.rb0 : 0) * T_ * a.ldg, q.nrow > 0);
+  };
+  auto load_g = [&](const Step& q, __amdgpu_buffer_rsrc_t rG, int c, tt_u32x4 (&gx)[3]) {
+    const uint32_t og = c * xc::CR + cr < q.nrow ? (uint32_t)(((c * xc::CR + cr) * T_ + q.t) * (int)a.ldg + j) * 2u
+                                                  : xc::OOB;
+#pragma unroll
+    for (int g = 0; g < 3; ++g) gx[g] = __builtin_amdgcn_raw_buffer_load_b128(rG, (int)og, g * H * 2, 0);
+  };
+  // h chunk c of step q (from the image of step idx - 1), or zeros at a round's first step
+  tt_u32x4 hv[C::QPW];
+  auto load_h = [&](const Step& q, int qidx, int c) {
+    if (q.s == 0) {
+#pragma unroll
+      for (int p = 0; p < C::QPW; ++p) hv[p] = tt_u32x4{0u, 0u, 0u, 0u};
+    } else {
+      xc_load_h<H>(rx[(qidx - 1) & 1], ho, c, hv);
+    }
+  };
+  float lr[8], lz[8], ln[8], hp[8];
+  auto read_gates = [&](int c, bool first) {  // first: h_{-1} = 0 (the round's state is stale)
+    const int rr = c * xc::CR + cr;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 v0 = *reinterpret_cast<const float4*>(stg + stg_off(cr, 0 * 64 + u0 + 4 * h));
+      const float4 v1 = *reinterpret_cast<const float4*>(stg + stg_off(cr, 1 * 64 + u0 + 4 * h));
+      const float4 v2 = *reinterpret_cast<const float4*>(stg + stg_off(cr, 2 * 64 + u0 + 4 * h));
+      const float4 p = *reinterpret_cast<const float4*>(stt + rr * xc::SSTR + u0 + 4 * h);
+      lr[4 * h] = v0.x; lr[4 * h + 1] = v0.y; lr[4 * h + 2] = v0.z; lr[4 * h + 3] = v0.w;
+      lz[4 * h] = v1.x; lz[4 * h + 1] = v1.y; lz[4 * h + 2] = v1.z; lz[4 * h + 3] = v1.w;
+      ln[4 * h] = v2.x; ln[4 * h + 1] = v2.y; ln[4 * h + 2] = v2.z; ln[4 * h + 3] = v2.w;
+      hp[4 * h] = first ? 0.f : p.x; hp[4 * h + 1] = first ? 0.f : p.y;
+      hp[4 * h + 2] = first ? 0.f : p.z; hp[4 * h + 3] = first ? 0.f : p.w;
+    }
+  };
+  f32x4 acc[2][3];
+  // ---- prologue: step 0's chunks 0-2 are zero h (slots zeroed), its gate inputs 0
+  for (int i = tid; i < 2 * C::SLOT / 16; i += xc::NT)
+    reinterpret_cast<float4*>(slots)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  Step cur = step_of(0);
+  __amdgpu_buffer_rsrc_t rGc = g_rsrc(cur);
+  tt_u32x4 gq[2][3];
+  load_g(cur, rGc, 0, gq[0]);
+#pragma unroll
+  for (int p = 0; p < C::QPW; ++p) hv[p] = tt_u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+  xc_mfma<H>(slots, wa, acc);
+  xc_stage(stg, acc);
+  __syncthreads();
+  read_gates(0, true);
+  for (int idx = 0; idx < NS; ++idx) {
+    const bool has_next = idx + 1 < NS;
+    const Step nxt = step_of(has_next ? idx + 1 : idx);
+    const __amdgpu_buffer_rsrc_t rGn = g_rsrc(nxt);
+    const long r0w = (long)(cur.nrow > 0 ? cur.rb0 : 0) * T_;
+    const bool on = cur.nrow > 0;
+    const __amdgpu_buffer_rsrc_t rY = tt_rsrc_n(Yw + r0w * a.ldy, on);
+    const __amdgpu_buffer_rsrc_t rX1 = tt_rsrc_n(X1 ? X1 + r0w * a.ldy : Yw, on && X1 != nullptr);
+    const __amdgpu_buffer_rsrc_t rS = tt_rsrc_n(S + r0w * 4L * H, on);
+    const __amdgpu_buffer_rsrc_t rdst_h = rx[idx & 1];
+    const int t = cur.t;
+#pragma unroll
+    for (int c = 0; c < xc::NCH; ++c) {
+      const bool more = c + 1 < xc::NCH || has_next;  // a chunk follows in the stream
+      // gate inputs of the next chunk (one ahead, two sets)
+      if (c + 1 < xc::NCH) load_g(cur, rGc, c + 1, gq[(c + 1) & 1]);
+      else if (has_next) load_g(nxt, rGn, 0, gq[0]);
+      {
+        const int rr = c * xc::CR + cr;
+        const bool ok = rr < cur.nrow;
+        float xr[8], xz[8], xn[8], y[8], sr[8], sz[8], sn[8], sg[8], msk[8];
+        const uint32_t grow = (uint32_t)(cur.rb0 + rr) * (uint32_t)T_ + (uint32_t)t;
+        const tt_u32x4(&gcur)[3] = gq[c & 1];
+        unpack8(make_uint4(gcur[0][0], gcur[0][1], gcur[0][2], gcur[0][3]), xr);
+        unpack8(make_uint4(gcur[1][0], gcur[1][1], gcur[1][2], gcur[1][3]), xz);
+        unpack8(make_uint4(gcur[2][0], gcur[2][1], gcur[2][2], gcur[2][3]), xn);
+        if (more) {  // the next chunk's MFMAs woven with this chunk's cells
+          const char* base = slots + ((c + 1) & 1) * C::SLOT + lane * 16;
+          auto frag = [&](int kt, int rb) { return *reinterpret_cast<const tt_u32x4*>(base + (kt * 2 + rb) * 1024); };
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int g = 0; g < 3; ++g) acc[rb][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+          tt_u32x4 f[3][2];
+          f[0][0] = frag(0, 0); f[0][1] = frag(0, 1);
+          f[1][0] = frag(1, 0); f[1][1] = frag(1, 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int kt = 0; kt < NKT; ++kt) {
+            if (kt + 2 < NKT) {
+              f[(kt + 2) % 3][0] = frag(kt + 2, 0);
+              f[(kt + 2) % 3][1] = frag(kt + 2, 1);
+            }
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+              for (int g = 0; g < 3; ++g)
+                acc[rb][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                    __builtin_bit_cast(bf16x8v, wa[g][kt]), __builtin_bit_cast(bf16x8v, f[kt % 3][rb]), acc[rb][g], 0, 0, 0);
+            if constexpr (DROP) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e)
+                if (e * NKT / 8 == kt) {
+                  msk[e] = tt_dropout_scale(R.seed, R.row0 + grow, (uint32_t)(R.col0 + j + e), a.drop_thresh, a.inv_keep);
+                  asm volatile("" : "+v"(msk[e]));
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if ((e + 1) * NKT / 8 - 1 == kt) {
+                asm volatile("" : "+v"(xr[e]), "+v"(xz[e]), "+v"(xn[e]), "+v"(lr[e]), "+v"(lz[e]), "+v"(ln[e]),
+                             "+v"(hp[e]));
+                gru_cell(xr[e], xz[e], xn[e], lr[e], lz[e], ln[e], bn[e], hp[e], y[e], sr[e], sz[e], sn[e], sg[e]);
+                asm volatile("" : "+v"(y[e]), "+v"(sr[e]), "+v"(sz[e]), "+v"(sn[e]), "+v"(sg[e]));
+              }
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, XC_VALU_PER_MFMA, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            gru_cell(xr[e], xz[e], xn[e], lr[e], lz[e], ln[e], bn[e], hp[e], y[e], sr[e], sz[e], sn[e], sg[e]);
+            if constexpr (DROP)
+              msk[e] = tt_dropout_scale(R.seed, R.row0 + grow, (uint32_t)(R.col0 + j + e), a.drop_thresh, a.inv_keep);
+          }
+        }
+        *reinterpret_cast<float4*>(stt + rr * xc::SSTR + u0) = make_float4(y[0], y[1], y[2], y[3]);
+        *reinterpret_cast<float4*>(stt + rr * xc::SSTR + u0 + 4) = make_float4(y[4], y[5], y[6], y[7]);
+        const uint4 yb = pack8bf(y);
+        if (fast) st16_buf(rdst_h, (uint32_t)(rr * H + j) * 2u, 0, yb);
+        else st16_buf_sc1(rdst_h, (uint32_t)(rr * H + j) * 2u, 0, yb);
+        asm volatile("" ::: "memory");  // exactly 6 stores follow (the publish below waits for the rest)
+        const int lrow = rr * T_ + t;
+        const uint32_t oy = ok ? (uint32_t)(lrow * (int)a.ldy + j) * 2u : xc::OOB;
+        const uint32_t os = ok ? (uint32_t)(lrow * 4 * H + j) * 2u : xc::OOB;
+        st16_buf(rY, oy, 0, yb);
+        st16_buf(rS, os, 0, pack8bf(sr));
+        st16_buf(rS, os, 2 * H, pack8bf(sz));
+        st16_buf(rS, os, 4 * H, pack8bf(sn));
+        st16_buf(rS, os, 6 * H, pack8bf(sg));
+        if constexpr (DROP) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) y[e] *= msk[e];
+          st16_buf(rX1, oy, 0, pack8bf(y));
+        } else {
+          st16_buf(rX1, oy, 0, yb);
+        }
+      }
+      // end of a half step: every wave's exchange stores done (only the six output stores
+      // after the last one may still be in flight); counted in after the barrier
+      if (c == 3 || c == 7) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      // h chunk two ahead into the slot this chunk's MFMAs used; request the one three ahead
+      if (c + 2 < xc::NCH || has_next) xc_put_h<H>(slots + (c & 1) * C::SLOT, hv);
+      if (c + 3 < xc::NCH) load_h(cur, idx, c + 3);
+      else if (has_next) load_h(nxt, idx + 1, c + 3 - xc::NCH);
+      // before the barrier: wait for the half step whose chunks are requested next
+      // iteration (chunk 4 of this step, chunk 0 of the next), also the write-after-read
+      // guard of the image half this member writes next
+      if (tid == 0) {
+        if (c == 0 && idx > 0) xc_wait(cntB, (unsigned)(M * idx), err);
+        if (c == 4 && has_next) xc_wait(cntA, (unsigned)(M * (idx + 1)), err);
+      }
+      __syncthreads();
+      if (tid == 0 && c == 3) __hip_atomic_fetch_add(cntA, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0 && c == 7) __hip_atomic_fetch_add(cntB, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (more) {
+        xc_stage(stg, acc);
+        __syncthreads();
+        if (c + 1 < xc::NCH) read_gates(c + 1, cur.s == 0);
+        else read_gates(0, nxt.s == 0);
+      }
+    }
+    cur = nxt;
+    rGc = rGn;
+  }
+}
+
 // ---- column-split persistent backward (gru_bwd_xc, bf16, H 256 / 512) ---------------
 // The BPTT of gru_fwd_xc's split (gru_bwd_rows' per-step math): member m of a group of
 // M = H/64 workgroups owns hidden units [64m, 64m+64) of the group's rows and keeps
@@ -3191,7 +3442,12 @@ static int gru_fwd_xc_launch(const FwdArgs& a, int nrec, int B, int T, int H, lo
   w.err = x->cnt + XC_MAX_GROUPS * xc::CSTR;
   TT_CHECK_HIP(hipMemsetAsync(x->cnt, 0, sizeof(unsigned) * ng * xc::CSTR, st));
   const bool drop = a.drop_thresh != 0 && a.r[0].x1 != nullptr;
-  if (H == 512 && drop) hipLaunchKernelGGL((gru_fwd_xc<512, true>), dim3(grid), dim3(xc::NT), 0, st, a, w);
+  if (!(tt::opt(tt::OPT_GRU_FWD_XC) & 8)) {  // the step-pipelined form (option bit 8: per-step waits)
+    if (H == 512 && drop) hipLaunchKernelGGL((gru_fwd_xcp<512, true>), dim3(grid), dim3(xc::NT), 0, st, a, w);
+    else if (H == 512) hipLaunchKernelGGL((gru_fwd_xcp<512, false>), dim3(grid), dim3(xc::NT), 0, st, a, w);
+    else if (drop) hipLaunchKernelGGL((gru_fwd_xcp<256, true>), dim3(grid), dim3(xc::NT), 0, st, a, w);
+    else hipLaunchKernelGGL((gru_fwd_xcp<256, false>), dim3(grid), dim3(xc::NT), 0, st, a, w);
+  } else if (H == 512 && drop) hipLaunchKernelGGL((gru_fwd_xc<512, true>), dim3(grid), dim3(xc::NT), 0, st, a, w);
   else if (H == 512) hipLaunchKernelGGL((gru_fwd_xc<512, false>), dim3(grid), dim3(xc::NT), 0, st, a, w);
   else if (drop) hipLaunchKernelGGL((gru_fwd_xc<256, true>), dim3(grid), dim3(xc::NT), 0, st, a, w);
   else hipLaunchKernelGGL((gru_fwd_xc<256, false>), dim3(grid), dim3(xc::NT), 0, st, a, w);

@@ -20,6 +20,7 @@ this host's cores.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import time
@@ -298,6 +299,11 @@ def main():
     timing.enabled = False
     kt = timing.summary()
     final_loss = float(loss.detach())
+    # the column-split GRU kernels' waits are bounded: a timeout would mean invalid outputs
+    flag = ctypes.c_int(0)
+    tta._lib.call("tt_gru_fwd_xc_status", ctypes.byref(flag))
+    if flag.value:
+        raise SystemExit("column-split GRU kernel wait timed out: outputs of the run are invalid")
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)

@@ -140,6 +140,9 @@ int tt_gru_fwd_launches(int dtype, int T, int H);
  * an internal per-device workspace, so one such forward per device at a time). Reports
  * and clears its wait-timeout flag (1: some launch's outputs are invalid); synchronises. */
 int tt_gru_fwd_xc_status(int* timed_out);
+/* Launches tt_gru_fwd issues for this exact call shape (1 where a column-split or
+ * row-owning persistent kernel applies, T for the per-step kernel); needs the device. */
+int tt_gru_fwd_launches_for(int dtype, int nrec, int B, int T, int H, long ldg, long ldy);
 
 /* Backward (BPTT) of tt_gru_fwd. Produces dL/dg (= dgx, feeds dWih, dbih and the
  * layer-input gradient) and dL/dgh (feeds dWhh), plus bias partial sums (one row per

@@ -108,6 +108,7 @@ _SIGS = {
     "tt_gru_bwd_launches": (c_int, [c_int, c_int, c_int]),
     "tt_gru_fwd_launches": (c_int, [c_int, c_int, c_int]),
     "tt_gru_fwd_xc_status": (c_int, [POINTER(c_int)]),
+    "tt_gru_fwd_launches_for": (c_int, [c_int, c_int, c_int, c_int, c_int, c_long, c_long]),
     "tt_proj_head_fwd": (c_int, [c_int, POINTER(HeadFwdIO), c_int, c_int, c_int, c_float, c_void_p]),
     "tt_proj_head_bwd": (c_int, [c_int, POINTER(HeadBwdIO), c_int, c_int, c_int, c_float, c_void_p]),
     "tt_proj_head_bwd_ws_size": (c_long, [c_int, c_int, c_int]),

@@ -2264,6 +2264,9 @@ __global__ __launch_bounds__(wr::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
 // Needs all groups resident at once: one workgroup per CU (the LDS use forbids two), grid =
 // 8 * M * (CUs / 8M) <= CUs; every wait is bounded (timeout flag, tt_gru_fwd_xc_status).
 typedef __attribute__((address_space(1))) unsigned xc_gu32;
+#ifndef XC_OUT_AUX
+#define XC_OUT_AUX 0
+#endif
 #ifndef XC_VALU_PER_MFMA
 #define XC_VALU_PER_MFMA 3
 #endif
@@ -2274,7 +2277,7 @@ constexpr int RR = 256;                // batch rows per round
 constexpr int NCH = RR / CR;           // chunks per round
 constexpr int SSTR = 68;               // LDS fp32 state row stride (64 units + 16 B pad)
 constexpr int STG = CR * 192 * 4;      // gate staging [32 rows][192 columns] fp32
-constexpr int CSTR = 32;               // arrival counters 128 B apart
+constexpr int CSTR = 64;               // per-group counter words (256 B): [0..2] counters, [8 + m] member XCDs (m < 32)
 constexpr unsigned OOB = 0x80000000u;  // buffer offset past num_records: load 0 / store dropped
 template <int H>
 struct Cfg {
@@ -2893,17 +2896,19 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
         const int lrow = rr * T_ + t;
         const uint32_t oy = ok ? (uint32_t)(lrow * (int)a.ldy + j) * 2u : xc::OOB;
         const uint32_t os = ok ? (uint32_t)(lrow * 4 * H + j) * 2u : xc::OOB;
-        st16_buf(rY, oy, 0, yb);
-        st16_buf(rS, os, 0, pack8bf(sr));
-        st16_buf(rS, os, 2 * H, pack8bf(sz));
-        st16_buf(rS, os, 4 * H, pack8bf(sn));
-        st16_buf(rS, os, 6 * H, pack8bf(sg));
+        // outputs: read only by later kernels (cache policy XC_OUT_AUX; offsets folded into
+        // the lane offset, soffset 0, as st16_buf does)
+        st16_buf_aux<XC_OUT_AUX>(rY, (int)oy, yb);
+        st16_buf_aux<XC_OUT_AUX>(rS, (int)os, pack8bf(sr));
+        st16_buf_aux<XC_OUT_AUX>(rS, (int)(os + 2u * H), pack8bf(sz));
+        st16_buf_aux<XC_OUT_AUX>(rS, (int)(os + 4u * H), pack8bf(sn));
+        st16_buf_aux<XC_OUT_AUX>(rS, (int)(os + 6u * H), pack8bf(sg));
         if constexpr (DROP) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) y[e] *= msk[e];
-          st16_buf(rX1, oy, 0, pack8bf(y));
+          st16_buf_aux<XC_OUT_AUX>(rX1, (int)oy, pack8bf(y));
         } else {
-          st16_buf(rX1, oy, 0, yb);
+          st16_buf_aux<XC_OUT_AUX>(rX1, (int)oy, yb);
         }
       }
       // end of a half step: every wave's exchange stores done (only the six output stores
@@ -2932,6 +2937,230 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
     }
     cur = nxt;
     rGc = rGn;
+  }
+}
+
+// ---- column-split forward for H 1024 (gru_fwd_xk, bf16; configs[4]'s hidden 512) -------
+// At H 1024 a 64-unit member's W_hh rows (192 x 1024, 384 KiB) exceed the accumulator
+// file, so a member owns 32 units (96 gate rows x 1024 = 192 KiB) and a group is 32
+// workgroups: one XCD. The 96 gate columns are 6 MFMA tiles, so the 4 waves split K
+// instead (256 each, 8 K-steps x 6 tiles = 192 AGPRs) and every LDS fragment is read by one
+// wave only; the four partial products meet in LDS and are summed in a fixed order by the
+// gate arithmetic (so results agree with the per-step kernel to rounding, not bitwise).
+// Rows in rounds of 256, chunks of 16 (h chunk image 32 KiB, double-buffered); every
+// thread updates 2 units of one row (the member's 32 units of a row are 64 bytes).
+// Exchange, counters, XCD check and the per-step wait as gru_fwd_xc.
+namespace xk {
+constexpr int NT = 256, CR = 16, RR = 256, NCH = RR / CR, NU = 32;
+constexpr int PSTR = 100;  // partial-product row stride in floats (96 + 4: conflict-free rows)
+constexpr int SSTR = 36;   // fp32 state row stride (32 units + 16 B)
+template <int H>
+struct Cfg {
+  static constexpr int M = H / NU;
+  static constexpr int NKW = H / 4 / 32;          // K-steps per wave
+  static constexpr int QPW = CR * H * 2 / 16 / NT;  // 16-byte h loads per thread and chunk
+  static constexpr int SLOT = CR * H * 2;
+  static constexpr int PST = 4 * CR * PSTR * 4;
+  static constexpr int ST = RR * SSTR * 4;
+  static constexpr int LDS = 2 * SLOT + PST + ST;
+};
+static_assert(Cfg<1024>::LDS <= 163840, "gru_fwd_xk LDS budget");
+}  // namespace xk
+
+template <int H, bool DROP>
+__global__ __launch_bounds__(xk::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gru_fwd_xk(FwdArgs a, XcWs ws) {
+  using C = xk::Cfg<H>;
+  constexpr int M = C::M, NKW = C::NKW, QPW = C::QPW;
+  __shared__ __attribute__((aligned(16))) char lds[C::LDS];
+  char* slots = lds;
+  float* pst = reinterpret_cast<float*>(lds + 2 * C::SLOT);
+  float* stt = reinterpret_cast<float*>(lds + 2 * C::SLOT + C::PST);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int xcd = blockIdx.x & 7, jj = blockIdx.x >> 3;
+  const int grp = xcd * ws.qg + jj / M, mem = jj % M;
+  const int rz = grp % ws.nrec, gi = grp / ws.nrec;
+  const FwdRec R = a.r[rz];
+  const int T_ = a.T, B = a.B;
+  const int gb0 = gi * ws.rpg;
+  xc_gu32* cnt = (xc_gu32*)(uintptr_t)(ws.cnt + grp * xc::CSTR);
+  xc_gu32* err = (xc_gu32*)(uintptr_t)ws.err;
+  bf16_t* xbg = ws.xb + (long)grp * 2 * xk::RR * H;
+  const __amdgpu_buffer_rsrc_t rx[2] = {tt_rsrc(xbg), tt_rsrc(xbg + xk::RR * H)};
+  // W_hh tile mt of this wave's K quarter: gate mt >> 1, units 32 mem + 16 (mt & 1) + lane&15
+  tt_u32x4 wa[6][NKW];
+  {
+    const bf16_t* W = static_cast<const bf16_t*>(R.whh);
+#pragma unroll
+    for (int mt = 0; mt < 6; ++mt)
+#pragma unroll
+      for (int ks = 0; ks < NKW; ++ks)
+        wa[mt][ks] = *reinterpret_cast<const tt_u32x4*>(
+            W + (long)((mt >> 1) * H + xk::NU * mem + 16 * (mt & 1) + (lane & 15)) * H + (wave * NKW + ks) * 32 +
+            (lane >> 4) * 8);
+#pragma unroll
+    for (int mt = 0; mt < 6; ++mt)
+#pragma unroll
+      for (int ks = 0; ks < NKW; ++ks) asm volatile("" : "+a"(wa[mt][ks]));
+  }
+  // h loads: 16-byte unit q = p * 256 + tid of the chunk image = K-step q >> 6, kq (q >> 4) & 3, row q & 15
+  const uint32_t xo0 = (uint32_t)(((tid & 15) * H + (tid >> 6) * 32 + ((tid >> 4) & 3) * 8) * 2);
+  // epilogue ownership: row er, units u0, u0+1 of the member's 32
+  const int er = tid >> 4, u0 = (tid & 15) * 2, j = xk::NU * mem + u0;
+  const float bn0 = R.bhn[j], bn1 = R.bhn[j + 1];
+  const bf16_t* G = static_cast<const bf16_t*>(R.g);
+  bf16_t* Yw = static_cast<bf16_t*>(R.y);
+  bf16_t* X1 = static_cast<bf16_t*>(R.x1);
+  bf16_t* S = static_cast<bf16_t*>(R.save);
+  const bool fast = xc_group_on_one_xcd(ws.cnt + grp * xc::CSTR, M, mem, ws.fast_ok != 0, err);
+  int idx = 0;
+  for (int r = 0; r < ws.nround; ++r) {
+    const int rb0 = gb0 + r * xk::RR;
+    const int nrow = min(min(ws.rpg - r * xk::RR, xk::RR), B - rb0);
+    const bool on = nrow > 0;
+    const long r0w = (long)(on ? rb0 : 0) * T_;
+    const __amdgpu_buffer_rsrc_t rG = tt_rsrc_n(G + r0w * a.ldg, on);
+    const __amdgpu_buffer_rsrc_t rY = tt_rsrc_n(Yw + r0w * a.ldy, on);
+    const __amdgpu_buffer_rsrc_t rX1 = tt_rsrc_n(X1 ? X1 + r0w * a.ldy : Yw, on && X1 != nullptr);
+    const __amdgpu_buffer_rsrc_t rS = tt_rsrc_n(S + r0w * 4L * H, on);
+    for (int i = tid; i < 2 * C::SLOT / 16; i += xk::NT)
+      reinterpret_cast<float4*>(slots)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = tid; i < C::ST / 16; i += xk::NT)
+      reinterpret_cast<float4*>(stt)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = 0; s < T_; ++s, ++idx) {
+      const int t = R.dir ? T_ - 1 - s : s;
+      const bool mm = s > 0;
+      if (idx > 0 && tid == 0) xc_wait(cnt, (unsigned)(M * idx), err);
+      __syncthreads();
+      const __amdgpu_buffer_rsrc_t rsrc = rx[(idx - 1) & 1];
+      const __amdgpu_buffer_rsrc_t rdst = rx[idx & 1];
+      tt_u32x4 hv[QPW];
+      auto load_h = [&](int c) {
+#pragma unroll
+        for (int p = 0; p < QPW; ++p)
+          hv[p] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(xo0 + p * 256), c * xk::CR * H * 2, 16);
+      };
+      auto put_h = [&](char* slot) {
+#pragma unroll
+        for (int p = 0; p < QPW; ++p) *reinterpret_cast<tt_u32x4*>(slot + tid * 16 + p * 4096) = hv[p];
+      };
+      f32x4 acc[6];
+      auto mfma = [&](const char* slot) {
+#pragma unroll
+        for (int mt = 0; mt < 6; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const char* base = slot + wave * NKW * 1024 + lane * 16;
+        tt_u32x4 f[3];
+        f[0] = *reinterpret_cast<const tt_u32x4*>(base);
+        f[1] = *reinterpret_cast<const tt_u32x4*>(base + 1024);
+#pragma unroll
+        for (int ks = 0; ks < NKW; ++ks) {
+          if (ks + 2 < NKW) f[(ks + 2) % 3] = *reinterpret_cast<const tt_u32x4*>(base + (ks + 2) * 1024);
+#pragma unroll
+          for (int mt = 0; mt < 6; ++mt)
+            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8v, wa[mt][ks]),
+                                                              __builtin_bit_cast(bf16x8v, f[ks % 3]), acc[mt], 0, 0, 0);
+        }
+      };
+      auto stage = [&]() {  // C^T: row lane & 15, columns 16 mt + 4 (lane >> 4) .. +3
+#pragma unroll
+        for (int mt = 0; mt < 6; ++mt)
+          *reinterpret_cast<f32x4*>(pst + (wave * xk::CR + (lane & 15)) * xk::PSTR + 16 * mt + 4 * (lane >> 4)) = acc[mt];
+      };
+      float gr[2], gz[2], gn[2];
+      auto read_part = [&]() {  // columns: gate g, unit u -> 32 g + u (tiles 2g, 2g+1)
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          float v[2] = {0.f, 0.f};
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const float2 q = *reinterpret_cast<const float2*>(pst + (w * xk::CR + er) * xk::PSTR + 32 * g + u0);
+            v[0] = w == 0 ? q.x : v[0] + q.x;
+            v[1] = w == 0 ? q.y : v[1] + q.y;
+          }
+          float* dst = g == 0 ? gr : g == 1 ? gz : gn;
+          dst[0] = v[0]; dst[1] = v[1];
+        }
+      };
+      uint32_t gx[3];
+      auto load_g = [&](int c) {
+        const int rr = c * xk::CR + er;
+        const uint32_t og = rr < nrow ? (uint32_t)((rr * T_ + t) * (int)a.ldg + j) * 2u : xc::OOB;
+#pragma unroll
+        for (int g = 0; g < 3; ++g) gx[g] = __builtin_amdgcn_raw_buffer_load_b32(rG, (int)og, g * H * 2, 0);
+      };
+      if (mm) {
+        load_h(0);
+        put_h(slots);
+        load_h(1);
+      }
+      load_g(0);
+      __syncthreads();
+      mfma(slots);
+      if (mm) {
+        put_h(slots + C::SLOT);
+        load_h(2);
+      }
+      stage();
+      __syncthreads();
+      read_part();
+#pragma unroll 1
+      for (int c = 0; c < xk::NCH; ++c) {
+        uint32_t gcur[3] = {gx[0], gx[1], gx[2]};
+        if (c + 1 < xk::NCH) {
+          load_g(c + 1);
+          mfma(slots + ((c + 1) & 1) * C::SLOT);
+        }
+        {
+          const int rr = c * xk::CR + er;
+          const bool ok = rr < nrow;
+          const float2 hpv = *reinterpret_cast<const float2*>(stt + rr * xk::SSTR + u0);
+          const float hp[2] = {hpv.x, hpv.y};
+          const float bn[2] = {bn0, bn1};
+          float y[2], sr[2], sz[2], sn[2], sg[2];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const float xr = __uint_as_float(e ? gcur[0] & 0xFFFF0000u : gcur[0] << 16);
+            const float xz = __uint_as_float(e ? gcur[1] & 0xFFFF0000u : gcur[1] << 16);
+            const float xn = __uint_as_float(e ? gcur[2] & 0xFFFF0000u : gcur[2] << 16);
+            gru_cell(xr, xz, xn, gr[e], gz[e], gn[e], bn[e], hp[e], y[e], sr[e], sz[e], sn[e], sg[e]);
+          }
+          *reinterpret_cast<float2*>(stt + rr * xk::SSTR + u0) = make_float2(y[0], y[1]);
+          auto pk2 = [](float a0, float a1) { return (uint32_t)f2bf(a0) | ((uint32_t)f2bf(a1) << 16); };
+          const uint32_t yb = pk2(y[0], y[1]);
+          if (fast) __builtin_amdgcn_raw_buffer_store_b32(yb, rdst, (int)((rr * H + j) * 2), 0, 0);
+          else __builtin_amdgcn_raw_buffer_store_b32(yb, rdst, (int)((rr * H + j) * 2), 0, 16);
+          const int lrow = rr * T_ + t;
+          const uint32_t oy = ok ? (uint32_t)(lrow * (int)a.ldy + j) * 2u : xc::OOB;
+          const uint32_t os = ok ? (uint32_t)(lrow * 4 * H + j) * 2u : xc::OOB;
+          __builtin_amdgcn_raw_buffer_store_b32(yb, rY, (int)oy, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(pk2(sr[0], sr[1]), rS, (int)os, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(pk2(sz[0], sz[1]), rS, (int)(os + 2u * H), 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(pk2(sn[0], sn[1]), rS, (int)(os + 4u * H), 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(pk2(sg[0], sg[1]), rS, (int)(os + 6u * H), 0, 0);
+          if constexpr (DROP) {
+            const uint32_t grow = (uint32_t)(rb0 + rr) * (uint32_t)T_ + (uint32_t)t;
+#pragma unroll
+            for (int e = 0; e < 2; ++e)
+              y[e] *= tt_dropout_scale(R.seed, R.row0 + grow, (uint32_t)(R.col0 + j + e), a.drop_thresh, a.inv_keep);
+            __builtin_amdgcn_raw_buffer_store_b32(pk2(y[0], y[1]), rX1, (int)oy, 0, 0);
+          } else {
+            __builtin_amdgcn_raw_buffer_store_b32(yb, rX1, (int)oy, 0, 0);
+          }
+        }
+        if (mm && c + 2 < xk::NCH) {
+          put_h(slots + (c & 1) * C::SLOT);
+          if (c + 3 < xk::NCH) load_h(c + 3);
+        }
+        __syncthreads();
+        if (c + 1 < xk::NCH) {
+          stage();
+          __syncthreads();
+          read_part();
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -3416,16 +3645,42 @@ extern "C" int tt_gru_fwd_xc_status(int* timed_out) {
   return 0;
 }
 
+// H 1024: gru_fwd_xk, 32 units per member, one group per XCD
+static bool xk_geometry(int H, int nrec, int B, int T, long ldg, long ldy, int cus, XcWs& w, int& grid) {
+  // opt-in (option gru_fwd_xc = 2 / 6): measured slower than the per-step kernel at
+  // configs[4] (63.3 vs 48.0 ms per layer; 16-row chunks)
+  const int v = tt::opt(tt::OPT_GRU_FWD_XC);
+  if ((v & 3) != 2 || H != 1024) return false;
+  if (tt::opt(tt::OPT_GRU_STEP) == 1) return false;
+  const int M = H / xk::NU;
+  const int qg = cus / (8 * M);
+  const int ng = 8 * qg;
+  if (qg < 1 || ng > XC_MAX_GROUPS || ng % nrec != 0) return false;
+  const int gpr = ng / nrec;
+  if ((v & 3) == 1 && (long)B < (long)gpr * (xk::RR / 2)) return false;
+  if ((long)xk::RR * T * std::max({4L * H, ldy, ldg}) * 2 >= (1L << 31)) return false;
+  w.qg = qg;
+  w.nrec = nrec;
+  w.rpg = tt_ceil_div(B, gpr);
+  w.nround = tt_ceil_div(w.rpg, xk::RR);
+  w.fast_ok = (v & 4) ? 0 : 1;
+  grid = ng * M;
+  return true;
+}
+
 static int gru_fwd_xc_launch(const FwdArgs& a, int nrec, int B, int T, int H, long ldg, long ldy, hipStream_t st,
                              bool* used) {
   *used = false;
-  if (tt::opt(tt::OPT_GRU_FWD_XC) == 0 || (H != 512 && H != 256)) return 0;
+  if (tt::opt(tt::OPT_GRU_FWD_XC) == 0 || (H != 512 && H != 256 && H != 1024)) return 0;
   XcDev* x = nullptr;
   TT_PROPAGATE(xc_device(&x));
   XcWs w{};
   int grid = 0;
-  if (!xc_geometry(TT_DT_BF16, H, nrec, B, T, ldg, ldy, x->cus, w, grid)) return 0;
-  const int ng = grid / (H / 64);
+  const bool k1024 = H == 1024;
+  if (k1024 ? !xk_geometry(H, nrec, B, T, ldg, ldy, x->cus, w, grid)
+            : !xc_geometry(TT_DT_BF16, H, nrec, B, T, ldg, ldy, x->cus, w, grid))
+    return 0;
+  const int ng = grid / (k1024 ? H / xk::NU : H / 64);
   {
     std::lock_guard<std::mutex> lock(g_xc_mu);
     const size_t need = (size_t)ng * 2 * xc::RR * H * sizeof(bf16_t);
@@ -3442,7 +3697,10 @@ static int gru_fwd_xc_launch(const FwdArgs& a, int nrec, int B, int T, int H, lo
   w.err = x->cnt + XC_MAX_GROUPS * xc::CSTR;
   TT_CHECK_HIP(hipMemsetAsync(x->cnt, 0, sizeof(unsigned) * ng * xc::CSTR, st));
   const bool drop = a.drop_thresh != 0 && a.r[0].x1 != nullptr;
-  if (!(tt::opt(tt::OPT_GRU_FWD_XC) & 8)) {  // the step-pipelined form (option bit 8: per-step waits)
+  if (k1024) {
+    if (drop) hipLaunchKernelGGL((gru_fwd_xk<1024, true>), dim3(grid), dim3(xk::NT), 0, st, a, w);
+    else hipLaunchKernelGGL((gru_fwd_xk<1024, false>), dim3(grid), dim3(xk::NT), 0, st, a, w);
+  } else if (!(tt::opt(tt::OPT_GRU_FWD_XC) & 8)) {  // the step-pipelined form (option bit 8: per-step waits)
     if (H == 512 && drop) hipLaunchKernelGGL((gru_fwd_xcp<512, true>), dim3(grid), dim3(xc::NT), 0, st, a, w);
     else if (H == 512) hipLaunchKernelGGL((gru_fwd_xcp<512, false>), dim3(grid), dim3(xc::NT), 0, st, a, w);
     else if (drop) hipLaunchKernelGGL((gru_fwd_xcp<256, true>), dim3(grid), dim3(xc::NT), 0, st, a, w);
@@ -3509,6 +3767,20 @@ static int gru_bwd_xc_launch(const BwdArgs& a, int nrec, int B, int T, int H, lo
   TT_CHECK_LAUNCH("gru_bwd_xc");
   *used = true;
   return 0;
+}
+
+extern "C" int tt_gru_fwd_launches_for(int dtype, int nrec, int B, int T, int H, long ldg, long ldy) {
+  if (dtype == TT_DT_BF16 && nrec >= 1 && nrec <= 4 && B > 0 && T > 0) {
+    XcDev* x = nullptr;
+    if (xc_device(&x) == 0) {
+      XcWs w{};
+      int grid = 0;
+      if (H == 1024 ? xk_geometry(H, nrec, B, T, ldg, ldy, x->cus, w, grid)
+                    : xc_geometry(dtype, H, nrec, B, T, ldg, ldy, x->cus, w, grid))
+        return 1;
+    }
+  }
+  return tt_gru_fwd_launches(dtype, T, H);
 }
 
 extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B, int T, int H, long ldg,

@@ -179,7 +179,7 @@ def _gru_layer_fwd(cfg, xs, K, ldx, packs, layer, B, T, seeds, want_x1):
     # algorithmic bytes per (row, unit, step): gates 3 + h 1 + saved 4 (+ dropout copy 1)
     # elements of dt; the per-step kernel also re-reads h_{s-1} (1 element) and moves the
     # fp32 recurrent state through HBM (8 B), the persistent one keeps both on chip
-    nl = _lib.load().tt_gru_fwd_launches(dtype_code(dt), T, H)
+    nl = _lib.load().tt_gru_fwd_launches_for(dtype_code(dt), 2 * n, B, T, H, 6 * H, 2 * H)
     per = esz * (8 + (1 if want_x1 else 0)) + (0 if nl == 1 else esz + 8)
     with timing.region("gru_fwd", nl, 2.0 * B * H * 3 * H * 2 * n * (T - 1), float(B * T * H * 2 * n * per)):
         call("tt_gru_fwd", dtype_code(dt), recs, 2 * n, B, T, H, 6 * H, 2 * H, cfg.drop_p if want_x1 else 0.0,

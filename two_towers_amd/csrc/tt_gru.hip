@@ -2947,22 +2947,23 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
 // instead (256 each, 8 K-steps x 6 tiles = 192 AGPRs) and every LDS fragment is read by one
 // wave only; the four partial products meet in LDS and are summed in a fixed order by the
 // gate arithmetic (so results agree with the per-step kernel to rounding, not bitwise).
-// Rows in rounds of 256, chunks of 16 (h chunk image 32 KiB, double-buffered); every
-// thread updates 2 units of one row (the member's 32 units of a row are 64 bytes).
+// Rows in rounds of 256, chunks of 32: ONE 64 KiB h chunk image in LDS (the next chunk
+// waits in registers and is written in right after the MFMAs that read the image); every
+// thread updates 4 units of one row (the member's 32 units of a row are 64 bytes).
 // Exchange, counters, XCD check and the per-step wait as gru_fwd_xc.
 namespace xk {
-constexpr int NT = 256, CR = 16, RR = 256, NCH = RR / CR, NU = 32;
+constexpr int NT = 256, CR = 32, RR = 256, NCH = RR / CR, NU = 32;
 constexpr int PSTR = 100;  // partial-product row stride in floats (96 + 4: conflict-free rows)
 constexpr int SSTR = 36;   // fp32 state row stride (32 units + 16 B)
 template <int H>
 struct Cfg {
   static constexpr int M = H / NU;
-  static constexpr int NKW = H / 4 / 32;          // K-steps per wave
+  static constexpr int NKW = H / 4 / 32;            // K-steps per wave
   static constexpr int QPW = CR * H * 2 / 16 / NT;  // 16-byte h loads per thread and chunk
-  static constexpr int SLOT = CR * H * 2;
+  static constexpr int SLOT = CR * H * 2;           // [K-step][row block][16 B x 64 lanes]
   static constexpr int PST = 4 * CR * PSTR * 4;
   static constexpr int ST = RR * SSTR * 4;
-  static constexpr int LDS = 2 * SLOT + PST + ST;
+  static constexpr int LDS = SLOT + PST + ST;
 };
 static_assert(Cfg<1024>::LDS <= 163840, "gru_fwd_xk LDS budget");
 }  // namespace xk
@@ -2972,9 +2973,9 @@ __global__ __launch_bounds__(xk::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
   using C = xk::Cfg<H>;
   constexpr int M = C::M, NKW = C::NKW, QPW = C::QPW;
   __shared__ __attribute__((aligned(16))) char lds[C::LDS];
-  char* slots = lds;
-  float* pst = reinterpret_cast<float*>(lds + 2 * C::SLOT);
-  float* stt = reinterpret_cast<float*>(lds + 2 * C::SLOT + C::PST);
+  char* slot = lds;
+  float* pst = reinterpret_cast<float*>(lds + C::SLOT);
+  float* stt = reinterpret_cast<float*>(lds + C::SLOT + C::PST);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int xcd = blockIdx.x & 7, jj = blockIdx.x >> 3;
   const int grp = xcd * ws.qg + jj / M, mem = jj % M;
@@ -3002,16 +3003,30 @@ __global__ __launch_bounds__(xk::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
 #pragma unroll
       for (int ks = 0; ks < NKW; ++ks) asm volatile("" : "+a"(wa[mt][ks]));
   }
-  // h loads: 16-byte unit q = p * 256 + tid of the chunk image = K-step q >> 6, kq (q >> 4) & 3, row q & 15
-  const uint32_t xo0 = (uint32_t)(((tid & 15) * H + (tid >> 6) * 32 + ((tid >> 4) & 3) * 8) * 2);
-  // epilogue ownership: row er, units u0, u0+1 of the member's 32
-  const int er = tid >> 4, u0 = (tid & 15) * 2, j = xk::NU * mem + u0;
-  const float bn0 = R.bhn[j], bn1 = R.bhn[j + 1];
+  // h loads: 16-byte unit q = p * 256 + tid of the chunk image = K-step q >> 7, row block
+  // (q >> 6) & 1, kq (q >> 4) & 3, row q & 15: piece p is 2 K-steps (128 B) further along
+  const uint32_t xo0 =
+      (uint32_t)(((((tid >> 6) & 1) * 16 + (tid & 15)) * H + (tid >> 7) * 32 + ((tid >> 4) & 3) * 8) * 2);
+  // epilogue ownership: row er, units u0 .. u0+3 of the member's 32
+  const int er = tid >> 3, u0 = (tid & 7) * 4, j = xk::NU * mem + u0;
+  float bn[4];
+  {
+    const float4 b4 = *reinterpret_cast<const float4*>(R.bhn + j);
+    bn[0] = b4.x; bn[1] = b4.y; bn[2] = b4.z; bn[3] = b4.w;
+  }
   const bf16_t* G = static_cast<const bf16_t*>(R.g);
   bf16_t* Yw = static_cast<bf16_t*>(R.y);
   bf16_t* X1 = static_cast<bf16_t*>(R.x1);
   bf16_t* S = static_cast<bf16_t*>(R.save);
   const bool fast = xc_group_on_one_xcd(ws.cnt + grp * xc::CSTR, M, mem, ws.fast_ok != 0, err);
+  auto st8b = [](__amdgpu_buffer_rsrc_t r, uint32_t off, uint2 v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), r,
+                                          (int)off, 0, 0);
+  };
+  auto pk4 = [](const float (&f)[4]) {
+    return make_uint2((uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16),
+                      (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16));
+  };
   int idx = 0;
   for (int r = 0; r < ws.nround; ++r) {
     const int rb0 = gb0 + r * xk::RR;
@@ -3022,8 +3037,8 @@ __global__ __launch_bounds__(xk::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
     const __amdgpu_buffer_rsrc_t rY = tt_rsrc_n(Yw + r0w * a.ldy, on);
     const __amdgpu_buffer_rsrc_t rX1 = tt_rsrc_n(X1 ? X1 + r0w * a.ldy : Yw, on && X1 != nullptr);
     const __amdgpu_buffer_rsrc_t rS = tt_rsrc_n(S + r0w * 4L * H, on);
-    for (int i = tid; i < 2 * C::SLOT / 16; i += xk::NT)
-      reinterpret_cast<float4*>(slots)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = tid; i < C::SLOT / 16; i += xk::NT)
+      reinterpret_cast<float4*>(slot)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int i = tid; i < C::ST / 16; i += xk::NT)
       reinterpret_cast<float4*>(stt)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int s = 0; s < T_; ++s, ++idx) {
@@ -3037,122 +3052,139 @@ __global__ __launch_bounds__(xk::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
       auto load_h = [&](int c) {
 #pragma unroll
         for (int p = 0; p < QPW; ++p)
-          hv[p] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(xo0 + p * 256), c * xk::CR * H * 2, 16);
+          hv[p] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(xo0 + p * 128), c * xk::CR * H * 2, 16);
       };
-      auto put_h = [&](char* slot) {
+      auto put_h = [&]() {
 #pragma unroll
         for (int p = 0; p < QPW; ++p) *reinterpret_cast<tt_u32x4*>(slot + tid * 16 + p * 4096) = hv[p];
       };
-      f32x4 acc[6];
-      auto mfma = [&](const char* slot) {
+      f32x4 acc[2][6];
+      auto mfma = [&]() {
 #pragma unroll
-        for (int mt = 0; mt < 6; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const char* base = slot + wave * NKW * 1024 + lane * 16;
-        tt_u32x4 f[3];
-        f[0] = *reinterpret_cast<const tt_u32x4*>(base);
-        f[1] = *reinterpret_cast<const tt_u32x4*>(base + 1024);
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+          for (int mt = 0; mt < 6; ++mt) acc[rb][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const char* base = slot + wave * NKW * 2048 + lane * 16;
+        tt_u32x4 f[2][2];
+        f[0][0] = *reinterpret_cast<const tt_u32x4*>(base);
+        f[0][1] = *reinterpret_cast<const tt_u32x4*>(base + 1024);
 #pragma unroll
         for (int ks = 0; ks < NKW; ++ks) {
-          if (ks + 2 < NKW) f[(ks + 2) % 3] = *reinterpret_cast<const tt_u32x4*>(base + (ks + 2) * 1024);
+          if (ks + 1 < NKW) {
+            f[(ks + 1) & 1][0] = *reinterpret_cast<const tt_u32x4*>(base + (ks + 1) * 2048);
+            f[(ks + 1) & 1][1] = *reinterpret_cast<const tt_u32x4*>(base + (ks + 1) * 2048 + 1024);
+          }
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int mt = 0; mt < 6; ++mt)
+              acc[rb][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  __builtin_bit_cast(bf16x8v, wa[mt][ks]), __builtin_bit_cast(bf16x8v, f[ks & 1][rb]), acc[rb][mt], 0, 0, 0);
+        }
+      };
+      auto stage = [&]() {  // C^T: row 16 rb + (lane & 15), columns 16 mt + 4 (lane >> 4) .. +3
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
           for (int mt = 0; mt < 6; ++mt)
-            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8v, wa[mt][ks]),
-                                                              __builtin_bit_cast(bf16x8v, f[ks % 3]), acc[mt], 0, 0, 0);
-        }
+            *reinterpret_cast<f32x4*>(pst + (wave * xk::CR + 16 * rb + (lane & 15)) * xk::PSTR + 16 * mt +
+                                      4 * (lane >> 4)) = acc[rb][mt];
       };
-      auto stage = [&]() {  // C^T: row lane & 15, columns 16 mt + 4 (lane >> 4) .. +3
-#pragma unroll
-        for (int mt = 0; mt < 6; ++mt)
-          *reinterpret_cast<f32x4*>(pst + (wave * xk::CR + (lane & 15)) * xk::PSTR + 16 * mt + 4 * (lane >> 4)) = acc[mt];
-      };
-      float gr[2], gz[2], gn[2];
-      auto read_part = [&]() {  // columns: gate g, unit u -> 32 g + u (tiles 2g, 2g+1)
+      float gh[3][4];
+      auto read_part = [&]() {  // column of gate g, unit u = 32 g + u; K quarters summed in order
 #pragma unroll
         for (int g = 0; g < 3; ++g) {
-          float v[2] = {0.f, 0.f};
+          float4 v = *reinterpret_cast<const float4*>(pst + (0 * xk::CR + er) * xk::PSTR + 32 * g + u0);
 #pragma unroll
-          for (int w = 0; w < 4; ++w) {
-            const float2 q = *reinterpret_cast<const float2*>(pst + (w * xk::CR + er) * xk::PSTR + 32 * g + u0);
-            v[0] = w == 0 ? q.x : v[0] + q.x;
-            v[1] = w == 0 ? q.y : v[1] + q.y;
+          for (int w = 1; w < 4; ++w) {
+            const float4 q = *reinterpret_cast<const float4*>(pst + (w * xk::CR + er) * xk::PSTR + 32 * g + u0);
+            v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
           }
-          float* dst = g == 0 ? gr : g == 1 ? gz : gn;
-          dst[0] = v[0]; dst[1] = v[1];
+          gh[g][0] = v.x; gh[g][1] = v.y; gh[g][2] = v.z; gh[g][3] = v.w;
         }
       };
-      uint32_t gx[3];
+      uint2 gx[3];
       auto load_g = [&](int c) {
         const int rr = c * xk::CR + er;
         const uint32_t og = rr < nrow ? (uint32_t)((rr * T_ + t) * (int)a.ldg + j) * 2u : xc::OOB;
 #pragma unroll
-        for (int g = 0; g < 3; ++g) gx[g] = __builtin_amdgcn_raw_buffer_load_b32(rG, (int)og, g * H * 2, 0);
+        for (int g = 0; g < 3; ++g) {
+          const auto w = __builtin_amdgcn_raw_buffer_load_b64(rG, (int)og, g * H * 2, 0);
+          gx[g] = make_uint2(w[0], w[1]);
+        }
       };
+      // prologue: chunk 0 into the image, chunk 1 in registers; MFMAs of chunk 0
       if (mm) {
         load_h(0);
-        put_h(slots);
+        put_h();
         load_h(1);
       }
       load_g(0);
       __syncthreads();
-      mfma(slots);
+      mfma();
+      __syncthreads();  // every wave done reading chunk 0's image
+      stage();
       if (mm) {
-        put_h(slots + C::SLOT);
+        put_h();
         load_h(2);
       }
-      stage();
       __syncthreads();
       read_part();
 #pragma unroll 1
       for (int c = 0; c < xk::NCH; ++c) {
-        uint32_t gcur[3] = {gx[0], gx[1], gx[2]};
+        const uint2 gcur[3] = {gx[0], gx[1], gx[2]};
+        const float gc[3][4] = {{gh[0][0], gh[0][1], gh[0][2], gh[0][3]},
+                                {gh[1][0], gh[1][1], gh[1][2], gh[1][3]},
+                                {gh[2][0], gh[2][1], gh[2][2], gh[2][3]}};
         if (c + 1 < xk::NCH) {
           load_g(c + 1);
-          mfma(slots + ((c + 1) & 1) * C::SLOT);
+          mfma();  // chunk c+1 from the image
         }
         {
           const int rr = c * xk::CR + er;
           const bool ok = rr < nrow;
-          const float2 hpv = *reinterpret_cast<const float2*>(stt + rr * xk::SSTR + u0);
-          const float hp[2] = {hpv.x, hpv.y};
-          const float bn[2] = {bn0, bn1};
-          float y[2], sr[2], sz[2], sn[2], sg[2];
+          const float4 hp4 = *reinterpret_cast<const float4*>(stt + rr * xk::SSTR + u0);
+          const float hp[4] = {hp4.x, hp4.y, hp4.z, hp4.w};
+          float y[4], sr[4], sz[4], sn[4], sg[4];
 #pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const float xr = __uint_as_float(e ? gcur[0] & 0xFFFF0000u : gcur[0] << 16);
-            const float xz = __uint_as_float(e ? gcur[1] & 0xFFFF0000u : gcur[1] << 16);
-            const float xn = __uint_as_float(e ? gcur[2] & 0xFFFF0000u : gcur[2] << 16);
-            gru_cell(xr, xz, xn, gr[e], gz[e], gn[e], bn[e], hp[e], y[e], sr[e], sz[e], sn[e], sg[e]);
+          for (int e = 0; e < 4; ++e) {
+            const uint32_t w0 = e < 2 ? gcur[0].x : gcur[0].y, w1 = e < 2 ? gcur[1].x : gcur[1].y,
+                           w2 = e < 2 ? gcur[2].x : gcur[2].y;
+            const float xr = __uint_as_float((e & 1) ? w0 & 0xFFFF0000u : w0 << 16);
+            const float xz = __uint_as_float((e & 1) ? w1 & 0xFFFF0000u : w1 << 16);
+            const float xn = __uint_as_float((e & 1) ? w2 & 0xFFFF0000u : w2 << 16);
+            gru_cell(xr, xz, xn, gc[0][e], gc[1][e], gc[2][e], bn[e], hp[e], y[e], sr[e], sz[e], sn[e], sg[e]);
           }
-          *reinterpret_cast<float2*>(stt + rr * xk::SSTR + u0) = make_float2(y[0], y[1]);
-          auto pk2 = [](float a0, float a1) { return (uint32_t)f2bf(a0) | ((uint32_t)f2bf(a1) << 16); };
-          const uint32_t yb = pk2(y[0], y[1]);
-          if (fast) __builtin_amdgcn_raw_buffer_store_b32(yb, rdst, (int)((rr * H + j) * 2), 0, 0);
-          else __builtin_amdgcn_raw_buffer_store_b32(yb, rdst, (int)((rr * H + j) * 2), 0, 16);
+          *reinterpret_cast<float4*>(stt + rr * xk::SSTR + u0) = make_float4(y[0], y[1], y[2], y[3]);
+          const uint2 yb = pk4(y);
+          const uint32_t ox = (uint32_t)(rr * H + j) * 2u;
+          if (fast) st8b(rdst, ox, yb);
+          else __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, yb), rdst, (int)ox, 0, 16);
           const int lrow = rr * T_ + t;
           const uint32_t oy = ok ? (uint32_t)(lrow * (int)a.ldy + j) * 2u : xc::OOB;
           const uint32_t os = ok ? (uint32_t)(lrow * 4 * H + j) * 2u : xc::OOB;
-          __builtin_amdgcn_raw_buffer_store_b32(yb, rY, (int)oy, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b32(pk2(sr[0], sr[1]), rS, (int)os, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b32(pk2(sz[0], sz[1]), rS, (int)(os + 2u * H), 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b32(pk2(sn[0], sn[1]), rS, (int)(os + 4u * H), 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b32(pk2(sg[0], sg[1]), rS, (int)(os + 6u * H), 0, 0);
+          st8b(rY, oy, yb);
+          st8b(rS, os, pk4(sr));
+          st8b(rS, os + 2u * H, pk4(sz));
+          st8b(rS, os + 4u * H, pk4(sn));
+          st8b(rS, os + 6u * H, pk4(sg));
           if constexpr (DROP) {
             const uint32_t grow = (uint32_t)(rb0 + rr) * (uint32_t)T_ + (uint32_t)t;
 #pragma unroll
-            for (int e = 0; e < 2; ++e)
+            for (int e = 0; e < 4; ++e)
               y[e] *= tt_dropout_scale(R.seed, R.row0 + grow, (uint32_t)(R.col0 + j + e), a.drop_thresh, a.inv_keep);
-            __builtin_amdgcn_raw_buffer_store_b32(pk2(y[0], y[1]), rX1, (int)oy, 0, 0);
+            st8b(rX1, oy, pk4(y));
           } else {
-            __builtin_amdgcn_raw_buffer_store_b32(yb, rX1, (int)oy, 0, 0);
+            st8b(rX1, oy, yb);
           }
         }
-        if (mm && c + 2 < xk::NCH) {
-          put_h(slots + (c & 1) * C::SLOT);
-          if (c + 3 < xk::NCH) load_h(c + 3);
-        }
-        __syncthreads();
+        __syncthreads();  // chunk c+1's image and chunk c's partial products fully read
         if (c + 1 < xk::NCH) {
           stage();
+          if (mm && c + 2 < xk::NCH) {
+            put_h();  // chunk c+2 into the image
+            if (c + 3 < xk::NCH) load_h(c + 3);
+          }
           __syncthreads();
           read_part();
         }

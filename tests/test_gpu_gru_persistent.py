@@ -255,8 +255,13 @@ def test_column_split_backward_matches_row_owning(H, B, T, ntow, dy):
     dYs = [(torch.randn(B * T, 2 * H, generator=g, device=DEV) * 0.05).to(torch.bfloat16) for _ in range(ntow)] if dy else None
     dfin = [torch.randn(B, 2 * H, generator=g, device=DEV) * 0.1 for _ in range(ntow)]
     dG_r, b_r = _run_bwd(ntow, B, T, H, S, Y, whh, dYs, dfin, 0)
+    # 2: L2-resident exchange images where a group shares an XCD; 6: write-through images
+    dG_w, b_w = _run_bwd(ntow, B, T, H, S, Y, whh, dYs, dfin, 6)
     dG_x, b_x = _run_bwd(ntow, B, T, H, S, Y, whh, dYs, dfin, 2)
     assert _xc_timed_out() == 0
+    for ti in range(ntow):  # the two exchange forms compute the same values
+        assert torch.equal(dG_w[ti].view(torch.int16), dG_x[ti].view(torch.int16))
+    assert torch.equal(b_w, b_x)
     for ti in range(ntow):
         for blk in range(8):
             a = dG_r[ti][:, blk * H:(blk + 1) * H]

@@ -86,13 +86,13 @@ def main():
             continue
         rows, dbg, strm = (v.split(":") + ["0", "2"])[:3]
         # P: gru_bwd_rows; R: gru_bwd_r64 with start delay `dbg` (gru_bwd_phase)
-        set_option("gru_bwd_persist", 1 if rows in ("P", "R", "X") else 0)
-        set_option("gru_bwd_xc", 2 if rows == "X" else 0)  # X: column-split gru_bwd_xc
+        set_option("gru_bwd_persist", 1 if rows in ("P", "R", "X", "W") else 0)
+        set_option("gru_bwd_xc", {"X": 2, "W": 6}.get(rows, 0))  # X / W: column-split gru_bwd_xc (W write-through)
         set_option("gru_bwd_r64", 1 if rows == "R" else 0)
         set_option("gru_bwd_phase", int(dbg) if rows == "R" else 0)
         # S: the 128x128 per-step kernels (gru_bwd_big = 0) with `strm` stream chains
         set_option("gru_bwd_big", 0 if rows == "S" else 1)
-        set_option("gru_bwd_rows", 128 if rows in ("P", "R", "S", "X") else int(rows))
+        set_option("gru_bwd_rows", 128 if rows in ("P", "R", "S", "X", "W") else int(rows))
         os.environ["TT_GRU_DBG"] = dbg  # read only by a -DTT_DIAG build
         set_option("gru_bwd_streams", int(strm))
         brecs, bkeep = setup_bwd(a.B, a.T, a.H, keep, dev)

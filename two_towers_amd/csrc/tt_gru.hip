@@ -3240,6 +3240,7 @@ struct XbWs {
   unsigned* cnt;
   unsigned* err;
   int qg, nrec, rpg, nround;
+  int fast_ok;
 };
 
 template <int H>
@@ -3302,6 +3303,7 @@ __global__ __launch_bounds__(xb::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
 #pragma unroll
     for (int e = 0; e < 4; ++e) bsum[q][e] = 0.f;
 
+  const bool fast = xc_group_on_one_xcd(ws.cnt + grp * xc::CSTR, M, mem, ws.fast_ok != 0, err);
 #ifdef TT_DIAG
   unsigned long long prf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   TT_STAMP(k_start);
@@ -3342,8 +3344,12 @@ __global__ __launch_bounds__(xb::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
       v[4] = make_uint2(wd[0], wd[1]);
       v[5] = make_uint2(wh[0], wh[1]);
     };
-    uint2 vcur[6], vnxt[6];
-    load_in(T_ - 1, 0, vcur);
+    // gate-arithmetic inputs: a ring of four chunk sets (chunk c in vq[c % 4]), requested
+    // three chunks ahead -- 16-row chunks are short next to HBM latency
+    uint2 vq[4][6];
+    load_in(T_ - 1, 0, vq[0]);
+    load_in(T_ - 1, 1, vq[1]);
+    load_in(T_ - 1, 2, vq[2]);
     for (int s = T_ - 1; s >= 0; --s, ++idx) {
       const int t = R.dir ? T_ - 1 - s : s;
       const bool last = s == T_ - 1;  // the first step processed: no recurrent gradient yet
@@ -3427,12 +3433,14 @@ __global__ __launch_bounds__(xb::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
       read_part(0);
       TT_STAMP(p2);
 #pragma unroll 1
-      for (int c = 0; c < xb::NCH; ++c) {
+      for (int c4 = 0; c4 < xb::NCH; c4 += 4)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = c4 + k;
+        const uint2(&vcur)[6] = vq[k];
         TT_STAMP(c0);
-        if (c + 1 < xb::NCH) {
-          load_in(s, c + 1, vnxt);
-          mfma(slots + ((c + 1) & 1) * C::SLOT);
-        }
+        if (c + 3 < xb::NCH) load_in(s, c + 3, vq[(k + 3) & 3]);
+        if (c + 1 < xb::NCH) mfma(slots + ((k + 1) & 1) * C::SLOT);
         {
           const int rr = c * xb::CR + er;
           float ar[4], az[4], an[4], gh[4], dy[4], hp[4];
@@ -3471,11 +3479,16 @@ __global__ __launch_bounds__(xb::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
           }
           // the exchange image: this member's r | z | W_hn h columns of the row
           const uint32_t ox = (uint32_t)(rr * 3 * H + j) * 2u;
-          tt_u32x4 w2;
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, br), rdst, (int)ox, 0, 16);
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, bz), rdst, (int)(ox + 2u * H), 0, 16);
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, bh), rdst, (int)(ox + 4u * H), 0, 16);
-          (void)w2;
+          typedef __attribute__((ext_vector_type(2))) unsigned u2v;
+          if (fast) {  // the image stays in the XCD's L2 (see gru_fwd_xc)
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, br), rdst, (int)ox, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, bz), rdst, (int)(ox + 2u * H), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, bh), rdst, (int)(ox + 4u * H), 0, 0);
+          } else {
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, br), rdst, (int)ox, 0, 16);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, bz), rdst, (int)(ox + 2u * H), 0, 16);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, bh), rdst, (int)(ox + 4u * H), 0, 16);
+          }
           const uint32_t og = ok && !(dbg & 2) ? (uint32_t)((rr * T_ + t) * (int)a.ldd + j) * 2u : xc::OOB;
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, br), rGX, (int)og, 0, 0);
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, bz), rGX, (int)(og + 2u * H), 0, 0);
@@ -3483,7 +3496,7 @@ __global__ __launch_bounds__(xb::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, bh), rGH, (int)og, 0, 0);
         }
         if (mm && c + 2 < xb::NCH) {
-          put_x(slots + (c & 1) * C::SLOT);
+          put_x(slots + (k & 1) * C::SLOT);
           if (c + 3 < xb::NCH) load_x(c + 3);
         }
         TT_STAMP(c1);
@@ -3492,8 +3505,6 @@ __global__ __launch_bounds__(xb::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
           stage();
           __syncthreads();
           read_part(c + 1);
-#pragma unroll
-          for (int q = 0; q < 6; ++q) vcur[q] = vnxt[q];
         }
         TT_STAMP(c2);
         TT_ACC(2, c1 - c0);
@@ -3503,7 +3514,11 @@ __global__ __launch_bounds__(xb::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
       if (!(dbg & 4)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (s > 0) load_in(s - 1, 0, vcur);
+      if (s > 0) {
+        load_in(s - 1, 0, vq[0]);
+        load_in(s - 1, 1, vq[1]);
+        load_in(s - 1, 2, vq[2]);
+      }
       TT_STAMP(p4);
       TT_ACC(0, p1 - p0);
       TT_ACC(1, p2 - p1);
@@ -3759,12 +3774,13 @@ static bool xb_geometry(int H, int nrec, int B, int T, long ldy, long ldd, int c
   if (qg < 1 || ng > XC_MAX_GROUPS || ng % nrec != 0) return false;
   const int gpr = ng / nrec;
   if (tt_gru_bias_rows(B) < gpr) return false;
-  if (v == 1 && (long)B < (long)gpr * (xb::RR / 2)) return false;
+  if ((v & 3) == 1 && (long)B < (long)gpr * (xb::RR / 2)) return false;
   if ((long)xb::RR * T * std::max({4L * H, ldy, ldd}) * 2 >= (1L << 31)) return false;
   w.qg = qg;
   w.nrec = nrec;
   w.rpg = tt_ceil_div(B, gpr);
   w.nround = tt_ceil_div(w.rpg, xb::RR);
+  w.fast_ok = (v & 4) ? 0 : 1;
   grid = ng * M;
   return true;
 }

@@ -358,3 +358,40 @@ def test_read_pairs_formats(tmp_path):
     assert pretok.read_pairs(str(tmp_path / "p.jsonl")) == (["q1", "q1", "q4"], ["b", "c", "d"])
     (tmp_path / "p.tsv").write_text("q1\tdoc one\nq2\tdoc\ttwo\n\n")
     assert pretok.read_pairs(str(tmp_path / "p.tsv")) == (["q1", "q2"], ["doc one", "doc\ttwo"])
+
+
+def test_column_split_publish_waits_cover_the_exchange_store():
+    """gru_fwd_xc / gru_fwd_xcp publish a (half) step after `s_waitcnt vmcnt(6)`: correct
+    only while the exchange-image store is followed by exactly the six output stores (Y, S
+    r / z / n / gh_n, X1) and nothing else of vector memory. Checked in the built gfx950
+    code of every instance (a compiler that moved a load or a store across would make the
+    members read an image that is not complete yet)."""
+    import importlib.util
+    import re
+    from two_towers_amd import _lib
+    if not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"):
+        pytest.skip("llvm-objdump not available")
+    spec = importlib.util.spec_from_file_location("chk", os.path.join(ROOT, "tools", "check_store_hazard.py"))
+    chk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(chk)
+    text = chk.disassemble(_lib.LIB_PATH)
+    funcs = re.split(r"\n(?=[0-9a-f]* ?<[^>]+>:)", text)
+    vmem = re.compile(r"^\s*(buffer|global|flat)_(load|store|atomic)\w*")
+    checked = 0
+    for f in funcs:
+        head = f.split("\n", 1)[0]
+        if "gru_fwd_xc" not in head:
+            continue
+        lines = f.split("\n")
+        # the publish waits are the asm pair `s_nop 0; s_waitcnt vmcnt(6)` (s_nop 0 marks them)
+        marks = {k + 1 for k in range(len(lines) - 1)
+                 if re.match(r"^\s*s_nop 0\b", lines[k]) and "s_waitcnt vmcnt(6)" in lines[k + 1]}
+        ops = [(k, ln) for k, ln in enumerate(lines) if vmem.match(ln) or k in marks]
+        for i, (k, ln) in enumerate(ops):
+            if k not in marks:
+                continue
+            before = [o for _, o in ops[:i] if vmem.match(o)][-7:]
+            assert len(before) == 7, head
+            assert all(re.match(r"^\s*buffer_store", o) for o in before), (head, before)
+            checked += 1
+    assert checked >= 8, checked  # xc: 1 per instance, xcp: 2 per instance (4 instances each)

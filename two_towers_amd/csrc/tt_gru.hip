@@ -2666,7 +2666,7 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
 #ifdef TT_DIAG
       if (!(a.dbg & 4))
 #endif
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // all but the last chunk's 6 output stores
+        asm volatile("s_nop 0\n\ts_waitcnt vmcnt(6)" ::: "memory");  // all but the last chunk's 6 output stores (s_nop 0: a marker for tests/test_host.py)
       __syncthreads();
       if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (s + 1 < T_) {
@@ -2913,7 +2913,7 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
       }
       // end of a half step: every wave's exchange stores done (only the six output stores
       // after the last one may still be in flight); counted in after the barrier
-      if (c == 3 || c == 7) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      if (c == 3 || c == 7) asm volatile("s_nop 0\n\ts_waitcnt vmcnt(6)" ::: "memory");  // s_nop 0: marker (test_host)
       // h chunk two ahead into the slot this chunk's MFMAs used; request the one three ahead
       if (c + 2 < xc::NCH || has_next) xc_put_h<H>(slots + (c & 1) * C::SLOT, hv);
       if (c + 3 < xc::NCH) load_h(cur, idx, c + 3);

@@ -20,7 +20,6 @@ this host's cores.
 from __future__ import annotations
 
 import argparse
-import ctypes
 import json
 import os
 import time
@@ -53,6 +52,9 @@ def parse():
     ap.add_argument("--cpu-batch", type=int, default=1024, help="pairs per CPU-baseline step (BASELINE.md plan)")
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--cpu-warmup", type=int, default=1)
+    ap.add_argument("--cpu-only", action="store_true",
+                    help="run only the CPU baseline (e.g. --cpu-batch 8192 --cpu-steps 2: the metric's batch) and "
+                         "print its JSON; bench lines attach the committed result (profiles/CPU_B8192)")
     ap.add_argument("--timing", action="store_true", help="print the per-kernel HIP-event table to stderr")
     return ap.parse_args()
 
@@ -145,21 +147,20 @@ def cpu_baseline(args):
 # hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1 KiB per dispatch, the gfx950 correction of
 # MI355X_MICROARCH.md). A region launch may cover several dispatches (the GRU backward
 # runs two chains of step kernels), hence the dispatches-per-step scaling.
-def _latest_pmc():
-    import glob
-    found = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*_pmc_summary.json")))
-    return found[-1] if found else ""
-
-
-PMC_SUMMARY = _latest_pmc()
-REGION_KERNEL = {"gru_bwd_step": ("gru_bwd_step<", "gru_bwd_big", "gru_bwd_rows<"), "gru_fwd": ("gru_fwd_seq<",),
+_HERE = os.path.dirname(os.path.abspath(__file__))
+# the PMC summary of the build this tree ships (tools/pmc_bench.sh), named explicitly
+PMC_SUMMARY = os.path.join(_HERE, "profiles", "r04_pmc_summary.json")
+# the CPU baseline at the metric's own batch (bench.py --cpu-only --cpu-batch 8192 --cpu-steps 2)
+CPU_B8192 = os.path.join(_HERE, "profiles", "r04_cpu_baseline_b8192.json")
+REGION_KERNEL = {"gru_bwd": ("gru_bwd_step<", "gru_bwd_big", "gru_bwd_rows<"), "gru_fwd": ("gru_fwd_xcp<", "gru_fwd_seq<"),
                  "embed_gather": ("embed_gather_kernel",)}
 
 
-def pmc_traffic(region, launches_per_step, args):
-    key = REGION_KERNEL.get(region)
+def pmc_traffic(region, kernel, launches_per_step, args):
+    """HBM bytes per launch of the region's kernel from the committed PMC summary."""
+    key = (kernel,) if kernel and kernel != region else REGION_KERNEL.get(region)
     if key is None or not os.path.exists(PMC_SUMMARY):
-        return {"traffic": None}
+        return {"traffic": None, "traffic_source": "no PMC summary of this build committed"}
     # the committed PMC passes (tools/pmc_bench.sh) run the default configs[2] workload
     if (args.emb, args.hidden, args.seq, args.batch, args.dtype, args.loss) != (300, 256, 64, 8192, "bf16",
                                                                                  "hardneg_margin"):
@@ -167,7 +168,7 @@ def pmc_traffic(region, launches_per_step, args):
     with open(PMC_SUMMARY) as f:
         summ = json.load(f)
     hits = [v for k, v in summ.items()
-            if any(s in k for s in key) and "hbm_bytes_est" in v and "dispatches_per_step" in v]
+            if any(k.startswith(s) for s in key) and "hbm_bytes_est" in v and "dispatches_per_step" in v]
     if not hits:
         return {"traffic": None}
     per_step = sum(v["hbm_bytes_est"] * v["dispatches_per_step"] for v in hits)
@@ -219,6 +220,9 @@ def spawn_local_ranks(n: int) -> int:
 
 def main():
     args = parse()
+    if args.cpu_only:
+        print(json.dumps(cpu_baseline(args)))
+        return
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         raise SystemExit(spawn_local_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -239,10 +243,10 @@ def main():
     import two_towers_amd as tta
     from two_towers_amd import dist as tdp
     if backend != "nccl" and world > max(torch.cuda.device_count(), 1):
-        # ranks sharing one GPU (gloo rehearsal): the column-split GRU kernels need every
-        # CU of the device for one launch, so two ranks' launches would only time out
+        # ranks sharing one GPU (gloo rehearsal only): the column-split GRU forward needs
+        # every CU of the device for one launch, and two processes' cooperative launches are
+        # not made co-resident with each other, so the rehearsal runs the row-owning forward
         tta._lib.set_option("gru_fwd_xc", 0)
-        tta._lib.set_option("gru_bwd_xc", 0)
     from two_towers_amd import timing
 
     if args.gpus != world:
@@ -299,11 +303,11 @@ def main():
     timing.enabled = False
     kt = timing.summary()
     final_loss = float(loss.detach())
-    # the column-split GRU kernels' waits are bounded: a timeout would mean invalid outputs
-    flag = ctypes.c_int(0)
-    tta._lib.call("tt_gru_fwd_xc_status", ctypes.byref(flag))
-    if flag.value:
-        raise SystemExit("column-split GRU kernel wait timed out: outputs of the run are invalid")
+    # the column-split GRU forward's waits are bounded: a timeout means invalid outputs
+    try:
+        tta.check_gru_status(wait=True)
+    except tta.GruTimeoutError as e:
+        raise SystemExit(f"invalid run: {e}")
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
@@ -337,10 +341,11 @@ def main():
         return out
 
     dom = max(kt, key=lambda k: kt[k]["ms_total"])
-    roofline = {"kernel": dom, **roof(dom), **pmc_traffic(dom, kt[dom]["launches"] / max(args.steps, 1), args)}
+    roofline = {"kernel": kt[dom]["kernel"], "region": dom, **roof(dom),
+                **pmc_traffic(dom, kt[dom]["kernel"], kt[dom]["launches"] / max(args.steps, 1), args)}
     extra = {k: roof(k) for k in kt if k != dom}
     step_ms = 1e3 * elapsed / args.steps
-    kernels = {k: {"ms_per_step": round(v["ms_total"] / args.steps, 3),
+    kernels = {k: {"kernel": v["kernel"], "ms_per_step": round(v["ms_total"] / args.steps, 3),
                    "tflops": round(v["work"] / (v["ms_total"] * 1e-3) / 1e12, 1) if k != "embed_gather" else None,
                    "gbs": round(v["bytes"] / (v["ms_total"] * 1e-3) / 1e9, 1)}
                for k, v in sorted(kt.items(), key=lambda kv: -kv[1]["ms_total"])}
@@ -351,6 +356,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
+        if os.path.exists(CPU_B8192):  # the metric's batch, measured separately (minutes of CPU time)
+            with open(CPU_B8192) as f:
+                cpu["at_metric_batch"] = {**json.load(f), "source": f"profiles/{os.path.basename(CPU_B8192)}"}
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,

@@ -40,9 +40,11 @@ const char* tt_version(void);
 const char* tt_last_error(void);
 /* Kernel-variant switches (process-wide; initialised once from the environment variable
  * of the same name in upper case with a TT_ prefix, e.g. gru_step <- TT_GRU_STEP):
- * gru_step, gru_depth, gru_stagger, gru_bwd_rows, gru_bwd_big, gru_bwd_streams,
- * gemm_persist, gemm_regstage, gemm_stream_out, hn_gemm, gru_bwd_persist. Every variant computes the
- * same function; they exist for A/B measurement and for tests that compare variants.
+ * gru_step, gru_depth, gru_bwd_rows, gru_bwd_big, gru_bwd_streams, gru_bwd_persist,
+ * gru_fwd_step_rows, gru_fwd_xc, gemm_persist, gemm_a3, gemm_regstage, gemm_stream_out,
+ * gemm_skew, gemm_persist_maxk, hn_gemm, hn_map, infonce_flash; diagnostics gru_xc_skip,
+ * gru_xc_spins. Every variant computes the same function; they exist for A/B measurement
+ * and for tests that compare variants.
  * Not synchronised with launches in flight: set them between steps. */
 int tt_set_option(const char* name, int value);
 int tt_get_option(const char* name, int* value);
@@ -129,28 +131,32 @@ typedef struct {
 } tt_gru_fwd_rec;
 
 int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B, int T, int H, long ldg,
-               long ldy, float drop_p, void* stream);
-/* Kernel launches tt_gru_fwd issues: 1 for the persistent bf16 kernel (H % 64 == 0,
- * H <= 512; 64 batch rows per workgroup kept resident for all T steps, hstate unused),
- * T for the per-step kernel (fp32, other H, or env TT_GRU_STEP=1). */
+               long ldy, float drop_p, void* ws, long ws_bytes, void* stream);
+/* Kernel launches tt_gru_fwd issues without a workspace: 1 for the persistent bf16 kernel
+ * (H % 64 == 0, H <= 512; 64 batch rows per workgroup kept resident for all T steps, hstate
+ * unused), T for the per-step kernel (fp32, other H, or option gru_step = 1). */
 int tt_gru_fwd_launches(int dtype, int T, int H);
-/* bf16, H 256 / 512, batch large enough (or option gru_fwd_xc = 2): tt_gru_fwd runs the
- * column-split persistent kernel instead (H/64 workgroups share a block of batch rows, each
- * keeps 64 units' W_hh rows in registers; h is exchanged between them every step through
- * an internal per-device workspace, so one such forward per device at a time). Reports
- * and clears its wait-timeout flag (1: some launch's outputs are invalid); synchronises. */
-int tt_gru_fwd_xc_status(int* timed_out);
-/* Launches tt_gru_fwd issues for this exact call shape (1 where a column-split or
- * row-owning persistent kernel applies, T for the per-step kernel); needs the device. */
+/* Device scratch (bytes, 0 = none used) that lets tt_gru_fwd run the column-split persistent
+ * kernel for this call shape on the current device: bf16, H 256 / 512, a batch large enough
+ * (or option gru_fwd_xc = 2), and every member workgroup co-resident (one per CU, checked
+ * against the occupancy query and launched cooperatively). H/64 workgroups share a block of
+ * batch rows, each keeps 64 units' W_hh rows in registers, and they exchange h every step
+ * through ws: per-group arrival counters (zeroed by every call, stream-ordered) and exchange
+ * images. ws: 256-byte aligned, one buffer per launch in flight (distinct streams need
+ * distinct buffers). NULL, or ws_bytes below the size: the row-owning kernel runs instead.
+ * The first 4 bytes of ws are a STATUS word: nonzero once a launch gave up waiting for a
+ * member (that launch's outputs are invalid). The library sets it and never clears it; the
+ * caller zeroes it when it allocates ws and reads it back (asynchronously) after the call. */
+long tt_gru_fwd_ws_size(int dtype, int nrec, int B, int T, int H, long ldg, long ldy);
+/* Launches tt_gru_fwd issues for this exact call shape given a tt_gru_fwd_ws_size workspace
+ * (1 where a column-split or row-owning persistent kernel applies, T for the per-step
+ * kernel); needs the device. */
 int tt_gru_fwd_launches_for(int dtype, int nrec, int B, int T, int H, long ldg, long ldy);
 
 /* Backward (BPTT) of tt_gru_fwd. Produces dL/dg (= dgx, feeds dWih, dbih and the
  * layer-input gradient) and dL/dgh (feeds dWhh), plus bias partial sums (one row per
- * 128-row batch tile, or per row group of the column-split kernel: tt_gru_bias_rows(B) >= 64
- * rows; columns r|z|n|ghn; reduce with tt_colsum: dbih = [0:3H], dbhh = [0:2H] ++ [3H:4H]).
- * bf16, H 256 / 512, batch large enough (or option gru_bwd_xc = 2): the column-split
- * persistent kernel (the BPTT of tt_gru_fwd's: H/64 workgroups exchange the step's gate
- * gradients through the same per-device workspace; dhstate unused). */
+ * 128-row batch tile: tt_gru_bias_rows(B) rows; columns r|z|n|ghn; reduce with tt_colsum:
+ * dbih = [0:3H], dbhh = [0:2H] ++ [3H:4H]). */
 typedef struct {
   const void* save;    /* [B*T, 4H] from tt_gru_fwd          */
   const void* y;       /* layer output (source of h_{s-1})   */

@@ -2,10 +2,13 @@
 
 BASELINE configs[2] runs EnhancedTwoTowerModel(300, 256) (GRU H = 512 per direction),
 seq_len 64, bf16, dropout 0.1, hard-negative mining k = 5 + MarginRankingLoss(0.2).
-These tests run exactly the kernels that step runs -- the persistent bf16 GRU forward
-(gru_fwd_seq<4, 8>), the row-owning BPTT kernel (gru_bwd_rows<512>, one launch per
-layer), the persistent input-projection GEMMs, the fp32 head, the hard-negative scan --
-at a batch the oracle finishes in seconds, and
+These tests run the kernels that step runs -- the column-split persistent GRU forward
+(gru_fwd_xcp<512, *>, which bench.py's B 8192 selects; forced here with option
+gru_fwd_xc = 2 because its auto mode needs B >= 1024 and the oracle wants a small batch)
+and the row-owning one it falls back to (gru_fwd_seq<4, 8>, the auto choice at these
+batches), the row-owning BPTT kernel (gru_bwd_rows<512>, one launch per layer), the
+persistent input-projection GEMMs, the fp32 head, the hard-negative scan -- at a batch
+the oracle finishes in seconds, and
 compare with oracle/cpu_ref.py (reference enhanced_two_tower.py:50-65, :67-82, :84-133)
 evaluated in fp32 on the same bf16-rounded weights and inputs, so only the kernels'
 internal bf16 rounding (operands of every MFMA, the saved pre-activations, the bf16
@@ -38,6 +41,7 @@ pytestmark = pytest.mark.gpu
 import two_towers_amd as tta  # noqa: E402
 from oracle import cpu_ref  # noqa: E402
 from two_towers_amd import _lib  # noqa: E402
+from two_towers_amd._lib import option  # noqa: E402
 
 DEV = "cuda"
 E, HID, T, B = 300, 256, 64, 256  # GRU H = 2 * HID = 512
@@ -69,19 +73,30 @@ def _grad_check(named, ref):
     return max(worst)
 
 
-@pytest.mark.parametrize("drop_p", [0.0, 0.1])
-def test_bench_config_bf16_matches_oracle(drop_p):
+def _xc_forced(xc):
+    """option gru_fwd_xc: 1 = auto (row-owning gru_fwd_seq at these batches), 2 = the
+    column-split gru_fwd_xcp forced; asserts which one the shape gets."""
     lib = _lib.load()
+    ws = lib.tt_gru_fwd_ws_size(_lib.DT_BF16, 4, B, T, 2 * HID, 6 * 2 * HID, 2 * 2 * HID)
+    assert (ws > 0) == (xc == 2), (xc, ws)
     assert lib.tt_gru_fwd_launches(_lib.DT_BF16, T, 2 * HID) == 1, "persistent forward expected at H=512"
+
+
+@pytest.mark.parametrize("xc", [1, 2])
+@pytest.mark.parametrize("drop_p", [0.0, 0.1])
+def test_bench_config_bf16_matches_oracle(drop_p, xc):
     m, p = _model(31)
     m.train() if drop_p > 0 else m.eval()
     g = torch.Generator().manual_seed(32)
     q = _bf16(torch.randn(B, T, E, generator=g) * 0.5)
     d = _bf16(torch.randn(B, T, E, generator=g) * 0.5)
     torch.manual_seed(33)  # the forward draws one dropout seed per tower from this stream
-    qv, dv = m(q.to(DEV), d.to(DEV))
-    loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
-    loss.backward()
+    with option("gru_fwd_xc", xc):
+        _xc_forced(xc)
+        qv, dv = m(q.to(DEV), d.to(DEV))
+        loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
+        loss.backward()
+    tta.check_gru_status()
     torch.manual_seed(33)
     seeds = [int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) for _ in range(2)] if drop_p > 0 else [0, 0]
     rq, rd = cpu_ref.forward(q, d, p, drop_p=drop_p, seeds=seeds)
@@ -163,7 +178,8 @@ def test_reference_size_h512_bf16_matches_oracle():
     print(f"h 512: loss {lv:.6f} vs {rv:.6f}; worst gradient {k}: rel {frob:.4f}, cos {cos:.5f}")
 
 
-def test_bench_composition_hardneg_margin_matches_oracle():
+@pytest.mark.parametrize("xc", [1, 2])
+def test_bench_composition_hardneg_margin_matches_oracle(xc):
     """The step bench.py times, end to end at B = 512: EnhancedTwoTowerModel(300, 256),
     T 64, bf16, dropout 0.1, HardNegativeMarginLoss (get_hard_negatives k = 5 over the
     in-batch documents + MarginRankingLoss(0.2) on the gathered rows,
@@ -177,7 +193,8 @@ def test_bench_composition_hardneg_margin_matches_oracle():
     the oracle's k-th best. Loss and gradients: given the GPU's picks, the oracle's margin
     loss through the oracle's forward/backward (so a differing near-tie pick is not counted
     as a gradient error): loss relative 5e-3, tower outputs as above, gradients with the
-    tolerances stated at the top of this file."""
+    tolerances stated at the top of this file. xc 2: with the column-split forward bench.py
+    runs at B 8192 (gru_fwd_xcp), forced at this batch."""
     Bq, k = 512, 5
     m, p = _model(41)
     m.train()
@@ -186,9 +203,13 @@ def test_bench_composition_hardneg_margin_matches_oracle():
     d = _bf16(torch.randn(Bq, T, E, generator=g) * 0.5)
     crit = tta.HardNegativeMarginLoss(k=k, margin=0.2, compute_dtype=torch.bfloat16)
     torch.manual_seed(43)
-    qv, dv = m(q.to(DEV), d.to(DEV))
-    loss = crit(qv, dv)
-    loss.backward()
+    with option("gru_fwd_xc", xc):
+        lib = _lib.load()
+        assert (lib.tt_gru_fwd_ws_size(_lib.DT_BF16, 4, Bq, T, 2 * HID, 6 * 2 * HID, 2 * 2 * HID) > 0) == (xc == 2)
+        qv, dv = m(q.to(DEV), d.to(DEV))
+        loss = crit(qv, dv)
+        loss.backward()
+    tta.check_gru_status()
     idx = crit.last_indices.long().cpu()
     torch.manual_seed(43)
     seeds = [int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) for _ in range(2)]

@@ -150,30 +150,6 @@ def test_cpu_tensors_fail_loudly():
         m(torch.randn(2, 3, 16), torch.randn(2, 3, 16))
 
 
-@pytest.mark.parametrize("h,B,T", [(128, 1100, 4), (256, 2048, 3)])
-def test_persistent_gru_staggered_block_order(h, B, T):
-    """Option gru_stagger = 1 (H 256 / 512 instances): each workgroup starts its unit-block
-    loop at (blockIdx / 8) mod nblk; same arithmetic per unit, so outputs and gradients
-    agree with the default order to fp32 rounding. B >= 1100 gives every offset."""
-    E = 48
-    g = torch.Generator().manual_seed(12)
-    q = torch.randn(B, T, E, generator=g).to(DEV)
-    d = torch.randn(B, T, E, generator=g).to(DEV)
-    outs = []
-    for stg in (0, 1):
-        m, _ = make_model(E, h, 3)
-        m = m.to(DEV).train().set_compute_dtype(torch.bfloat16)
-        with option("gru_stagger", stg):
-            qv, dv = m(q, d)
-            loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
-            loss.backward()
-        outs.append((qv.detach().clone(), dv.detach().clone(), {k: p.grad.clone() for k, p in m.named_parameters()}))
-    (q0, d0, g0), (q1, d1, g1) = outs
-    assert rel(q1, q0) < 1e-5 and rel(d1, d0) < 1e-5
-    for k in g0:
-        assert rel(g1[k], g0[k]) < 1e-4, k
-
-
 @pytest.mark.parametrize("h,B,T", [(32, 96, 10), (64, 200, 7), (128, 70, 4), (256, 130, 5)])
 def test_persistent_gru_matches_step_kernel(h, B, T):
     """bf16 forward + backward through the persistent (row-resident) GRU forward
@@ -189,33 +165,6 @@ def test_persistent_gru_matches_step_kernel(h, B, T):
         m, _ = make_model(E, h, 3)
         m = m.to(DEV).train().set_compute_dtype(torch.bfloat16)
         with option("gru_step", step):
-            qv, dv = m(q, d)
-            loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
-            loss.backward()
-        outs.append((qv.detach().clone(), dv.detach().clone(), {k: p.grad.clone() for k, p in m.named_parameters()}))
-    (q0, d0, g0), (q1, d1, g1) = outs
-    assert torch.equal(q1, q0) and torch.equal(d1, d0)
-    for k in g0:
-        assert torch.equal(g1[k], g0[k]), (k, rel(g1[k], g0[k]))
-
-
-@pytest.mark.parametrize("rr", [1, 2, 3])
-def test_experimental_row_resident_forward_is_bit_identical(rr):
-    """Option gru_fwd_rr (the 128-row forward with the gates in registers, measured slower
-    and off by default): same MFMA order along K and the same gate expression as
-    gru_fwd_seq, so the forward outputs are bit-identical, and so are the gradients (every
-    reduction on the InfoNCE path runs in a fixed order). B = 130 gives a tail tile of 2
-    rows; dropout on."""
-    E, h, B, T = 48, 256, 130, 5
-    g = torch.Generator().manual_seed(13)
-    q = torch.randn(B, T, E, generator=g).to(DEV)
-    d = torch.randn(B, T, E, generator=g).to(DEV)
-    outs = []
-    for v in (0, rr):
-        m, _ = make_model(E, h, 3)
-        m = m.to(DEV).train().set_compute_dtype(torch.bfloat16)
-        with option("gru_fwd_rr", v):
-            torch.manual_seed(5)
             qv, dv = m(q, d)
             loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
             loss.backward()
@@ -274,12 +223,10 @@ def test_big_tile_gru_backward_matches_step_kernel(B, T):
         assert cos > 0.9999 and rel(outs[1][k], outs[0][k]) < 2e-2, (k, cos)
 
 
-@pytest.mark.parametrize("r64", [0, 1])
 @pytest.mark.parametrize("h,B,T", [(256, 130, 5), (256, 520, 3), (128, 200, 6)])
-def test_row_owning_gru_backward_matches_step_kernels(h, B, T, r64):
-    """bf16 backward through the persistent row-owning kernels (one launch per layer,
-    H 512 / 256: gru_bwd_rows, 128 rows x all H units per workgroup; r64: gru_bwd_r64,
-    64 rows per workgroup, two per CU, second half of the grid started late) vs the
+def test_row_owning_gru_backward_matches_step_kernels(h, B, T):
+    """bf16 backward through the persistent row-owning kernel (one launch per layer,
+    H 512 / 256: gru_bwd_rows, 128 rows x all H units per workgroup) vs the
     per-step launches (option gru_bwd_persist = 0): the same arithmetic per element, so
     gradients agree to accumulation order (the recurrent GEMM's K order and the bias
     partial sums differ). B 130 / 520 / 200 give tail row tiles."""
@@ -291,7 +238,7 @@ def test_row_owning_gru_backward_matches_step_kernels(h, B, T, r64):
     for persist in (0, 1):
         m, _ = make_model(E, h, 5)
         m = m.to(DEV).train().set_compute_dtype(torch.bfloat16)
-        with option("gru_bwd_persist", persist), option("gru_bwd_r64", r64), option("gru_bwd_phase", 2 * r64):
+        with option("gru_bwd_persist", persist):
             qv, dv = m(q, d)
             loss = tta.InfoNCELoss(compute_dtype=torch.bfloat16)(qv, dv)
             loss.backward()

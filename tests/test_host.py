@@ -361,11 +361,16 @@ def test_read_pairs_formats(tmp_path):
 
 
 def test_column_split_publish_waits_cover_the_exchange_store():
-    """gru_fwd_xc / gru_fwd_xcp publish a (half) step after `s_waitcnt vmcnt(6)`: correct
-    only while the exchange-image store is followed by exactly the six output stores (Y, S
-    r / z / n / gh_n, X1) and nothing else of vector memory. Checked in the built gfx950
-    code of every instance (a compiler that moved a load or a store across would make the
-    members read an image that is not complete yet)."""
+    """gru_fwd_xcp publishes a half step after `s_waitcnt vmcnt(6)`: correct only while the
+    exchange-image store is followed by exactly the six output stores (Y, S r / z / n /
+    gh_n, X1) and nothing else of vector memory. Checked in the built gfx950 code of every
+    instance, with the exchange store identified, not just counted: it is the one store
+    the kernel issues in two forms (plain where the group shares an XCD, write-through
+    `sc1` otherwise, on the two sides of a branch), so the 7th vector-memory op before
+    each marked wait must be that `sc1` store, the 8th its plain twin (same address and
+    resource registers), and none of the six after it may use its resource (a compiler
+    that moved an output store in front of it would leave the exchange store inside the
+    six in flight, and the members could read an incomplete image)."""
     import importlib.util
     import re
     from two_towers_amd import _lib
@@ -377,12 +382,13 @@ def test_column_split_publish_waits_cover_the_exchange_store():
     text = chk.disassemble(_lib.LIB_PATH)
     funcs = re.split(r"\n(?=[0-9a-f]* ?<[^>]+>:)", text)
     vmem = re.compile(r"^\s*(buffer|global|flat)_(load|store|atomic)\w*")
+    store = re.compile(r"^\s*buffer_store_dwordx4 v\[\d+:\d+\], (v\d+), (s\[\d+:\d+\]), 0 offen(.*)$")
     checked = 0
     for f in funcs:
         head = f.split("\n", 1)[0]
         if "gru_fwd_xc" not in head:
             continue
-        lines = f.split("\n")
+        lines = [ln.split("//")[0].rstrip() for ln in f.split("\n")]
         # the publish waits are the asm pair `s_nop 0; s_waitcnt vmcnt(6)` (s_nop 0 marks them)
         marks = {k + 1 for k in range(len(lines) - 1)
                  if re.match(r"^\s*s_nop 0\b", lines[k]) and "s_waitcnt vmcnt(6)" in lines[k + 1]}
@@ -390,8 +396,13 @@ def test_column_split_publish_waits_cover_the_exchange_store():
         for i, (k, ln) in enumerate(ops):
             if k not in marks:
                 continue
-            before = [o for _, o in ops[:i] if vmem.match(o)][-7:]
-            assert len(before) == 7, head
-            assert all(re.match(r"^\s*buffer_store", o) for o in before), (head, before)
+            before = [o for _, o in ops[:i] if vmem.match(o)][-8:]
+            assert len(before) == 8, head
+            m = [store.match(o) for o in before]
+            assert all(m), (head, before)
+            plain, wt, outs = m[0], m[1], m[2:]
+            assert "sc1" in wt.group(3) and "sc1" not in plain.group(3), (head, before[:2])
+            assert (plain.group(1), plain.group(2)) == (wt.group(1), wt.group(2)), (head, before[:2])
+            assert all(o.group(2) != wt.group(2) and "sc1" not in o.group(3) for o in outs), (head, before)
             checked += 1
-    assert checked >= 8, checked  # xc: 1 per instance, xcp: 2 per instance (4 instances each)
+    assert checked >= 8, checked  # 2 half-step publishes per instance, 4 instances

@@ -67,32 +67,37 @@ def setup_bwd(B, T, H, keep, dev):
     return recs, (dY, dfin, dG, dhs, part)
 
 
+def fwd_call(recs, a, st, ws):
+    call("tt_gru_fwd", 1, recs, 4, a.B, a.T, a.H, 6 * a.H, 2 * a.H, 0.1,
+         ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0, st)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--B", type=int, default=8192)
     ap.add_argument("--T", type=int, default=64)
     ap.add_argument("--H", type=int, default=512)
     ap.add_argument("--iters", type=int, default=3)
-    ap.add_argument("--variants", default="seq:0")
-    ap.add_argument("--bwd-variants", default="128:0:2")
-    ap.add_argument("--check", default="", help="kind:kind - compare Y / X1 / S of two forward kinds")
+    ap.add_argument("--variants", default="xc:0,seq:0",
+                    help="kind:dbg[:depth]; kind xc (column-split, forced), xcs (write-through exchange), "
+                         "xcx (members dealt over XCDs), seq (row-owning), step (per-step)")
+    ap.add_argument("--bwd-variants", default="P:0:2", help="rows:dbg:streams; rows P (row-owning), S (128x128 "
+                    "per-step, `streams` chains), 128 / 64 (per-step 256x256 / 128-row tiles)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     recs, keep = setup(a.B, a.T, a.H, dev)
     st = stream_ptr(dev)
-    call("tt_gru_fwd", 1, recs, 4, a.B, a.T, a.H, 6 * a.H, 2 * a.H, 0.1, st)  # real S / Y for the backward
+    set_option("gru_fwd_xc", 2)
+    nb = _lib.load().tt_gru_fwd_ws_size(1, 4, a.B, a.T, a.H, 6 * a.H, 2 * a.H)
+    ws = torch.zeros(max(nb, 256), dtype=torch.uint8, device=dev) if nb else None
+    fwd_call(recs, a, st, ws)  # real S / Y for the backward
     for v in a.bwd_variants.split(","):
         if not v:
             continue
         rows, dbg, strm = (v.split(":") + ["0", "2"])[:3]
-        # P: gru_bwd_rows; R: gru_bwd_r64 with start delay `dbg` (gru_bwd_phase)
-        set_option("gru_bwd_persist", 1 if rows in ("P", "R", "X", "W") else 0)
-        set_option("gru_bwd_xc", {"X": 2, "W": 6}.get(rows, 0))  # X / W: column-split gru_bwd_xc (W write-through)
-        set_option("gru_bwd_r64", 1 if rows == "R" else 0)
-        set_option("gru_bwd_phase", int(dbg) if rows == "R" else 0)
-        # S: the 128x128 per-step kernels (gru_bwd_big = 0) with `strm` stream chains
+        set_option("gru_bwd_persist", 1 if rows == "P" else 0)
         set_option("gru_bwd_big", 0 if rows == "S" else 1)
-        set_option("gru_bwd_rows", 128 if rows in ("P", "R", "S", "X", "W") else int(rows))
+        set_option("gru_bwd_rows", 128 if rows in ("P", "S") else int(rows))
         os.environ["TT_GRU_DBG"] = dbg  # read only by a -DTT_DIAG build
         set_option("gru_bwd_streams", int(strm))
         brecs, bkeep = setup_bwd(a.B, a.T, a.H, keep, dev)
@@ -108,36 +113,15 @@ def main():
         ms = s.elapsed_time(e) / a.iters
         print(json.dumps({"bwd_rows": v, "ms": round(ms, 3)}), flush=True)
         del brecs, bkeep
-    if a.check:
-        outs = []
-        for kind in a.check.split(":"):
-            set_option("gru_step", 1 if kind == "step" else 0)
-            set_option("gru_fwd_rr", {"rr": 1, "rr2": 2, "rr3": 3}.get(kind, 0))
-            set_option("gru_fwd_wr", 1 if kind == "wr" else 0)
-            set_option("gru_fwd_pair", {"pair": 1, "ew": 2, "ds": 3, "ds2": 4, "tm": 5, "s16": 6}.get(kind, 0))
-            set_option("gru_depth", 4)
-            set_option("gru_fwd_xc", 2 if kind == "xc" else 0)
-            for t in keep[3] + keep[4] + [x for p in keep[5] for x in p]:
-                t.fill_(float("nan"))
-            call("tt_gru_fwd", 1, recs, 4, a.B, a.T, a.H, 6 * a.H, 2 * a.H, 0.1, st)
-            torch.cuda.synchronize()
-            outs.append([t.float().clone() for t in keep[3] + keep[4] + [x for p in keep[5] for x in p]])
-        for name, x, y in zip(["Y0", "Y1", "X1_0", "X1_1", "S00", "S01", "S10", "S11"], *outs):
-            d = (x - y).abs()
-            print(json.dumps({"check": a.check, "out": name, "nan": int(torch.isnan(y).sum()), "max_abs": float(d.max()),
-                              "n_diff": int((d > 0).sum()), "ref_max": float(x.abs().max())}), flush=True)
     for v in a.variants.split(","):
         if not v:
             continue
         kind, dbg, *depth = v.split(":")
         set_option("gru_step", 1 if kind == "step" else 0)
-        set_option("gru_fwd_rr", {"rr": 1, "rr2": 2, "rr3": 3}.get(kind, 0))
-        set_option("gru_fwd_wr", 1 if kind == "wr" else 0)
-        set_option("gru_fwd_pair", {"pair": 1, "ew": 2, "ds": 3, "ds2": 4, "tm": 5, "s16": 6}.get(kind, 0))
         os.environ["TT_GRU_DBG"] = dbg  # read only by a -DTT_DIAG build
         set_option("gru_depth", int(depth[0]) if depth else 4)
-        set_option("gru_fwd_xc", {"xc": 2, "xcs": 6, "xco": 10}.get(kind, 0))
-        f = lambda: call("tt_gru_fwd", 1, recs, 4, a.B, a.T, a.H, 6 * a.H, 2 * a.H, 0.1, st)
+        set_option("gru_fwd_xc", {"xc": 2, "xcs": 6, "xcx": 18}.get(kind, 0))
+        f = lambda: fwd_call(recs, a, st, ws if kind.startswith("xc") else None)
         f()
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -148,7 +132,9 @@ def main():
         torch.cuda.synchronize()
         ms = s.elapsed_time(e) / a.iters
         gb = a.B * a.T * a.H * 4 * 18 / 1e9
-        print(json.dumps({"variant": v, "ms": round(ms, 3), "alg_GBs_18B": round(gb / (ms * 1e-3), 1)}), flush=True)
+        status = int(ws[:4].view(torch.int32).item()) if ws is not None else 0
+        print(json.dumps({"variant": v, "ms": round(ms, 3), "alg_GBs_18B": round(gb / (ms * 1e-3), 1),
+                          "xc_status": status}), flush=True)
 
 
 if __name__ == "__main__":

@@ -12,11 +12,13 @@ from .margin import MarginIdDataset, SimpleDataset, TwoTowerModel, margin_ids
 from .losses import HardNegativeMarginLoss, InfoNCELoss, MarginRankingLoss, get_hard_negatives, mine_hard_negatives
 from .model import EnhancedTwoTower, EnhancedTwoTowerModel
 from .optim import Adam
+from ._lib import GruTimeoutError
+from .towers import check_gru_status
 
 __all__ = [
     "EnhancedTwoTowerModel", "EnhancedTwoTower", "InfoNCELoss", "MarginRankingLoss", "HardNegativeMarginLoss",
     "get_hard_negatives", "mine_hard_negatives", "EnhancedDataset", "EnhancedIdDataset", "MSMarcoDataset",
     "Vocab", "encode_ids", "encode_batch", "load_word2vec", "load_ms_marco_train", "pairs_from_msmarco", "Adam",
-    "TwoTowerModel", "SimpleDataset", "MarginIdDataset", "margin_ids",
+    "TwoTowerModel", "SimpleDataset", "MarginIdDataset", "margin_ids", "check_gru_status", "GruTimeoutError",
 ]
 __version__ = "0.1.0"

@@ -24,6 +24,11 @@ class TTError(RuntimeError):
     pass
 
 
+class GruTimeoutError(TTError):
+    """A column-split GRU forward launch gave up waiting for one of its member workgroups
+    (tt_gru_fwd's status word): that launch's outputs are invalid."""
+
+
 class GemmBatch(ctypes.Structure):
     _fields_ = [
         ("a", c_void_p * 4),
@@ -101,13 +106,13 @@ _SIGS = {
     "tt_gemm_ws_size": (c_long, [c_int, c_int, c_int, c_int]),
     "tt_gemm_pick_splits": (c_int, [c_int, c_int, c_int, c_int]),
     "tt_gru_fwd": (c_int, [c_int, POINTER(GruFwdRec), c_int, c_int, c_int, c_int, c_long, c_long, c_float,
-                           c_void_p]),
+                           c_void_p, c_long, c_void_p]),
     "tt_gru_bwd": (c_int, [c_int, POINTER(GruBwdRec), c_int, c_int, c_int, c_int, c_long, c_long, c_long,
                            c_void_p]),
     "tt_gru_bias_rows": (c_int, [c_int]),
     "tt_gru_bwd_launches": (c_int, [c_int, c_int, c_int]),
     "tt_gru_fwd_launches": (c_int, [c_int, c_int, c_int]),
-    "tt_gru_fwd_xc_status": (c_int, [POINTER(c_int)]),
+    "tt_gru_fwd_ws_size": (c_long, [c_int, c_int, c_int, c_int, c_int, c_long, c_long]),
     "tt_gru_fwd_launches_for": (c_int, [c_int, c_int, c_int, c_int, c_int, c_long, c_long]),
     "tt_proj_head_fwd": (c_int, [c_int, POINTER(HeadFwdIO), c_int, c_int, c_int, c_float, c_void_p]),
     "tt_proj_head_bwd": (c_int, [c_int, POINTER(HeadBwdIO), c_int, c_int, c_int, c_float, c_void_p]),

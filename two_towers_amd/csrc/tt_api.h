@@ -15,7 +15,6 @@ void set_error(const char* fmt, ...);
 enum Opt {
   OPT_GRU_STEP,         // 1: per-step GRU forward even where the persistent kernel applies
   OPT_GRU_DEPTH,        // persistent forward W_hh ring depth cap (1, 2, 4)
-  OPT_GRU_STAGGER,      // persistent forward: staggered W_hh block order (fixed-NKT instances)
   OPT_GRU_BWD_ROWS,     // 128 or 64 batch rows per backward step tile
   OPT_GRU_BWD_BIG,      // 0: 128x128 backward step kernels instead of 256x256
   OPT_GRU_BWD_STREAMS,  // 1: one stream chain for the 128x128 backward
@@ -25,18 +24,15 @@ enum Opt {
   OPT_GEMM_STREAM_OUT,  // 0: no write-through output stores
   OPT_HN_GEMM,          // 1: hard-negative top-k through GEMM + split top-k, no scan
   OPT_GRU_BWD_PERSIST,  // 0: per-step backward launches instead of the row-owning kernel
-  OPT_GRU_BWD_R64,      // 1: row-owning backward with 64-row workgroups, two per CU
-  OPT_GRU_BWD_PHASE,    // gru_bwd_r64: start delay of the grid's second half (s_sleep 127 units)
   OPT_GRU_FWD_STEP_ROWS, // per-step GRU forward batch rows per tile: 128, 256 (0: by size)
   OPT_INFONCE_FLASH,    // 0: InfoNCE backward through a materialised dS (bf16, h 128/256 default fused)
-  OPT_GRU_FWD_RR,       // 1/2/3: experimental 128-row forward with gates in registers (bf16, H 512)
-  OPT_GRU_FWD_WR,       // 1: wave-owned-rows persistent forward (bf16, H 256 / 512; h in registers)
   OPT_HN_MAP,           // hn_scan block -> (row tile, split) map: 0 split per XCD, 1 row tile per XCD
   OPT_GEMM_SKEW,        // persistent GEMM: start workgroup w after (w % 4) * skew * 4096 cycles
   OPT_GEMM_PERSIST_MAXK,  // persistent GEMM for problems of at most this many K-tiles
-  OPT_GRU_FWD_PAIR,     // persistent forward: two K-tiles per barrier (4-stage W_hh ring)
-  OPT_GRU_FWD_XC,       // column-split persistent forward: 0 off, 1 where the batch fills it, 2 wherever it applies
-  OPT_GRU_BWD_XC,       // column-split persistent backward (experiment, off by default: measured slower): 1 where the batch fills it, 2 wherever it applies
+  OPT_GRU_FWD_XC,       // column-split persistent forward: 0 off, 1 where the batch fills it, 2 wherever it
+                        // applies (+4: write-through exchange images; +16: members dealt across XCDs)
+  OPT_GRU_XC_SKIP,      // diagnostic: member m-1 of group 0 never publishes (0: off); the others' waits time out
+  OPT_GRU_XC_SPINS,     // column-split wait bound: log2 of the poll count before a wait gives up (default 22)
   OPT_N
 };
 int opt(Opt o);

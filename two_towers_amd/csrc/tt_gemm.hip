@@ -27,18 +27,16 @@ struct OptDef {
   int dflt;
 };
 constexpr OptDef kOpts[OPT_N] = {
-    {"gru_step", "TT_GRU_STEP", 0},         {"gru_depth", "TT_GRU_DEPTH", 4},
-    {"gru_stagger", "TT_GRU_STAGGER", 0},   {"gru_bwd_rows", "TT_GRU_BWD_ROWS", 128},
-    {"gru_bwd_big", "TT_GRU_BWD_BIG", 1},   {"gru_bwd_streams", "TT_GRU_BWD_STREAMS", 2},
-    {"gemm_persist", "TT_GEMM_PERSIST", 1}, {"gemm_a3", "TT_GEMM_A3", 1}, {"gemm_regstage", "TT_GEMM_REGSTAGE", 0},
+    {"gru_step", "TT_GRU_STEP", 0},               {"gru_depth", "TT_GRU_DEPTH", 4},
+    {"gru_bwd_rows", "TT_GRU_BWD_ROWS", 128},     {"gru_bwd_big", "TT_GRU_BWD_BIG", 1},
+    {"gru_bwd_streams", "TT_GRU_BWD_STREAMS", 2}, {"gemm_persist", "TT_GEMM_PERSIST", 1},
+    {"gemm_a3", "TT_GEMM_A3", 1},                 {"gemm_regstage", "TT_GEMM_REGSTAGE", 0},
     {"gemm_stream_out", "TT_GEMM_STREAM_OUT", 1}, {"hn_gemm", "TT_HN_GEMM", 0},
-    {"gru_bwd_persist", "TT_GRU_BWD_PERSIST", 1}, {"gru_bwd_r64", "TT_GRU_BWD_R64", 0},
-    {"gru_bwd_phase", "TT_GRU_BWD_PHASE", 0},     {"gru_fwd_step_rows", "TT_GRU_FWD_STEP_ROWS", 0},
-    {"infonce_flash", "TT_INFONCE_FLASH", 1},     {"gru_fwd_rr", "TT_GRU_FWD_RR", 0},
-    {"gru_fwd_wr", "TT_GRU_FWD_WR", 0},           {"hn_map", "TT_HN_MAP", 0},
+    {"gru_bwd_persist", "TT_GRU_BWD_PERSIST", 1}, {"gru_fwd_step_rows", "TT_GRU_FWD_STEP_ROWS", 0},
+    {"infonce_flash", "TT_INFONCE_FLASH", 1},     {"hn_map", "TT_HN_MAP", 0},
     {"gemm_skew", "TT_GEMM_SKEW", 0},             {"gemm_persist_maxk", "TT_GEMM_PERSIST_MAXK", 24},
-    {"gru_fwd_pair", "TT_GRU_FWD_PAIR", 0},       {"gru_fwd_xc", "TT_GRU_FWD_XC", 1},
-    {"gru_bwd_xc", "TT_GRU_BWD_XC", 0},
+    {"gru_fwd_xc", "TT_GRU_FWD_XC", 1},           {"gru_xc_skip", "TT_GRU_XC_SKIP", 0},
+    {"gru_xc_spins", "TT_GRU_XC_SPINS", 22},
 };
 struct OptTable {
   std::atomic<int> v[OPT_N];

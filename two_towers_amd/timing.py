@@ -14,19 +14,24 @@ import torch
 
 enabled = False
 _records = defaultdict(list)
+_kernels = {}
 
 
 def reset():
     _records.clear()
+    _kernels.clear()
 
 
 @contextmanager
-def region(name: str, launches: int, work: float, nbytes: float = 0.0):
+def region(name: str, launches: int, work: float, nbytes: float = 0.0, kernel: str | None = None):
     """work = algorithmic FLOPs (or bytes for pure data movement), nbytes =
-    algorithmic HBM bytes of the region (inputs read once + outputs written once)."""
+    algorithmic HBM bytes of the region (inputs read once + outputs written once),
+    kernel = the name of the kernel the region launches (as rocprofv3 prints it)."""
     if not enabled:
         yield
         return
+    if kernel:
+        _kernels[name] = kernel
     s = torch.cuda.Event(enable_timing=True)
     e = torch.cuda.Event(enable_timing=True)
     s.record()
@@ -45,5 +50,6 @@ def summary():
         w = sum(r[3] for r in recs)
         b = sum(r[4] for r in recs)
         out[name] = dict(ms_total=ms, launches=n, work=w, bytes=b, ms_per_launch=ms / max(n, 1),
-                         work_per_launch=w / max(n, 1), bytes_per_launch=b / max(n, 1), calls=len(recs))
+                         work_per_launch=w / max(n, 1), bytes_per_launch=b / max(n, 1), calls=len(recs),
+                         kernel=_kernels.get(name, name))
     return out

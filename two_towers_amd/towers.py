@@ -18,6 +18,7 @@ Layout in HBM (per tower; row = b*T + t, dt = compute dtype):
 from __future__ import annotations
 
 import ctypes
+import threading
 from dataclasses import dataclass
 
 import torch
@@ -117,6 +118,66 @@ def _alloc(shape, dt, dev):
     return torch.empty(shape, dtype=dt, device=dev)
 
 
+# ---- column-split GRU forward: caller-owned workspace and its status word --------------
+# tt_gru_fwd runs the column-split kernel (member workgroups that exchange h every step)
+# only with a workspace from the caller (include/tt_hip.h tt_gru_fwd_ws_size). Its first
+# word is a status the kernels set when a member wait timed out -- the launch's outputs
+# are then invalid. After each forward the word is copied to pinned host memory on the
+# stream (no device synchronisation); check_gru_status() raises GruTimeoutError for any
+# such launch. TowersFn.forward checks every earlier forward (waiting on its event: the
+# host is at most the GPU's queue ahead, which still holds later work, so the GPU never
+# idles for it), TowersFn.backward the ones already finished.
+_status_lock = threading.Lock()
+_status_pending: list = []  # (event, pinned int32[1])
+
+
+def gru_fwd_workspace(nrec, B, T, H, dt, dev):
+    """Zero-status workspace for one tt_gru_fwd call shape, or None when the column-split
+    kernel does not apply (tt_gru_fwd then runs the row-owning kernel without one)."""
+    nb = _lib.load().tt_gru_fwd_ws_size(dtype_code(dt), nrec, B, T, H, 6 * H, 2 * H)
+    if nb <= 0:
+        return None
+    ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+    if ws.data_ptr() % 256:
+        raise _lib.TTError("GRU forward workspace is not 256-byte aligned")
+    ws[:256].zero_()
+    return ws
+
+
+def watch_gru_status(ws):
+    """Queue an asynchronous read-back of ws's status word (after the launches using it)."""
+    host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+    host.copy_(ws[:4].view(torch.int32), non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    with _status_lock:
+        _status_pending.append((ev, host))
+
+
+def check_gru_status(wait: bool = True):
+    """Raise GruTimeoutError if a watched column-split forward gave up a member wait.
+    wait=False checks only the launches that have already finished."""
+    with _status_lock:
+        pend = list(_status_pending)
+        _status_pending.clear()
+    bad = 0
+    keep = []
+    for ev, host in pend:
+        if not wait and not ev.query():
+            keep.append((ev, host))
+            continue
+        ev.synchronize()
+        bad += int(host.item() != 0)
+    if keep:
+        with _status_lock:
+            _status_pending[:0] = keep
+    if bad:
+        raise _lib.GruTimeoutError(
+            f"{bad} column-split GRU forward launch(es) timed out waiting for a member workgroup "
+            "(not all workgroups were resident); their outputs are invalid. Set option gru_fwd_xc=0 "
+            "(env TT_GRU_FWD_XC=0) to use the row-owning kernel.")
+
+
 def table_cols(table, x):
     return getattr(table, "real_cols", table.shape[1])
 
@@ -144,7 +205,7 @@ def featurize(x: torch.Tensor, table: torch.Tensor | None, Ep: int, dt: torch.dt
     return out
 
 
-def _gru_layer_fwd(cfg, xs, K, ldx, packs, layer, B, T, seeds, want_x1):
+def _gru_layer_fwd(cfg, xs, K, ldx, packs, layer, B, T, seeds, want_x1, ws):
     """Input projection + one bidirectional GRU layer for every tower. The dropout copy
     X1 (want_x1) draws keep(seed, rank*B*T + b*T + t, col): on N data-parallel ranks the
     masks are those the single-process run of the global batch draws."""
@@ -179,11 +240,19 @@ def _gru_layer_fwd(cfg, xs, K, ldx, packs, layer, B, T, seeds, want_x1):
     # algorithmic bytes per (row, unit, step): gates 3 + h 1 + saved 4 (+ dropout copy 1)
     # elements of dt; the per-step kernel also re-reads h_{s-1} (1 element) and moves the
     # fp32 recurrent state through HBM (8 B), the persistent one keeps both on chip
-    nl = _lib.load().tt_gru_fwd_launches_for(dtype_code(dt), 2 * n, B, T, H, 6 * H, 2 * H)
+    nl = _lib.load().tt_gru_fwd_launches_for(dtype_code(dt), 2 * n, B, T, H, 6 * H, 2 * H) if ws is not None \
+        else _lib.load().tt_gru_fwd_launches(dtype_code(dt), T, H)
     per = esz * (8 + (1 if want_x1 else 0)) + (0 if nl == 1 else esz + 8)
-    with timing.region("gru_fwd", nl, 2.0 * B * H * 3 * H * 2 * n * (T - 1), float(B * T * H * 2 * n * per)):
+    if nl == 1 and ws is not None:
+        kname = f"gru_fwd_xcp<{H}, {'true' if want_x1 and cfg.drop_p > 0 else 'false'}>"
+    elif nl == 1:
+        kname = "gru_fwd_seq<"
+    else:
+        kname = "gru_fwd_step<"
+    with timing.region("gru_fwd", nl, 2.0 * B * H * 3 * H * 2 * n * (T - 1), float(B * T * H * 2 * n * per),
+                       kernel=kname):
         call("tt_gru_fwd", dtype_code(dt), recs, 2 * n, B, T, H, 6 * H, 2 * H, cfg.drop_p if want_x1 else 0.0,
-             stream_ptr(dev))
+             ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0, stream_ptr(dev))
     del G
     return Y, X1, S
 
@@ -220,7 +289,10 @@ def _gru_layer_bwd(cfg, layer, B, T, S, Y, dY, dfinal, packs):
     esz = 2 if dt == torch.bfloat16 else 4
     nl = lib.tt_gru_bwd_launches(dtype_code(dt), T, H)
     per = esz * (14 + (1 if dY is not None else 0))
-    with timing.region("gru_bwd_step", nl, 2.0 * B * 3 * H * H * 2 * n * (T - 1), float(B * T * H * 2 * n * per)):
+    kname = (f"gru_bwd_rows<{H}>" if nl == 1 else
+             "gru_bwd_big" if dt == torch.bfloat16 and H % 256 == 0 and _lib.get_option("gru_bwd_big") else "gru_bwd_step<")
+    with timing.region("gru_bwd", nl, 2.0 * B * 3 * H * H * 2 * n * (T - 1), float(B * T * H * 2 * n * per),
+                       kernel=kname):
         call("tt_gru_bwd", dtype_code(dt), recs, 2 * n, B, T, H, 2 * H, 8 * H, ldf, stream_ptr(dev))
     sums = _alloc((n * 2, 4 * H), torch.float32, dev)
     for i in range(2 * n):
@@ -270,6 +342,7 @@ class TowersFn(torch.autograd.Function):
         n = cfg.ntowers
         xs, params = args[:n], args[n:]
         _lib.require_gpu(*xs, *params)
+        check_gru_status(wait=True)  # every earlier forward's column-split launches
         dt, E, H, h = cfg.dtype, cfg.E, cfg.H, cfg.h
         dev = xs[0].device
         B, T = xs[0].shape[0], xs[0].shape[1]
@@ -282,9 +355,13 @@ class TowersFn(torch.autograd.Function):
         X0 = [featurize(x, table, Ep, dt) for x in xs]
         train_drop = cfg.drop_p > 0.0
         seeds = [int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) for _ in range(n)] if train_drop else [0] * n
-        Y0, X1, S0 = _gru_layer_fwd(cfg, X0, Ep, Ep, packs, 0, B, T, seeds, train_drop)
+        # one workspace for both layers (same shape; the launches are stream-ordered)
+        ws = gru_fwd_workspace(2 * n, B, T, H, dt, dev)
+        Y0, X1, S0 = _gru_layer_fwd(cfg, X0, Ep, Ep, packs, 0, B, T, seeds, train_drop, ws)
         Xl1 = X1 if train_drop else Y0
-        Y1, _, S1 = _gru_layer_fwd(cfg, Xl1, 2 * H, 2 * H, packs, 1, B, T, seeds, False)
+        Y1, _, S1 = _gru_layer_fwd(cfg, Xl1, 2 * H, 2 * H, packs, 1, B, T, seeds, False, ws)
+        if ws is not None:
+            watch_gru_status(ws)
         # cat(h_fwd at t=T-1, h_rev at t=0) -> [B, 2H] (enhanced_two_tower.py:53,59)
         hcat = []
         for ti in range(n):
@@ -321,6 +398,7 @@ class TowersFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, *gouts):
         cfg = ctx.cfg
+        check_gru_status(wait=False)  # the forwards that have finished by now
         n, dt, E, H, h = cfg.ntowers, cfg.dtype, cfg.E, cfg.H, cfg.h
         B, T, Ep = ctx.dims
         packs = ctx.packs

@@ -1,16 +1,17 @@
 #!/bin/bash
-# hn_scan A/B: product vs experiment library, rocprofv3 kernel stats over tools/bench_score.py hardneg.
-# Usage: tools/ab_scan.sh TAG
+# hn_scan A/B: rocprofv3 kernel stats over tools/bench_score.py hardneg for each library.
+# Usage: tools/ab_scan.sh TAG [lib.so ...]   (default: libtt_hip.so libtt_hip_exp.so)
 set -o pipefail
-TAG=${1:-x}
+TAG=${1:-x}; shift
+LIBS=${@:-libtt_hip.so libtt_hip_exp.so}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/abscan_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-for rep in 1 2; do for lib in libtt_hip.so libtt_hip_exp.so; do
+for rep in 1 2; do for lib in $LIBS; do
   TT_HIP_LIB=$ROOT/two_towers_amd/lib/$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv \
     -d $OUT/${lib%.so}_$rep -o p -- python $ROOT/tools/bench_score.py --ops hardneg --iters 20 \
-    > $OUT/${lib%.so}_$rep.log 2>&1 || { echo "prof $lib $rep failed"; exit 1; }
+    --hn-shapes 8192x8192x256,8192x65536x256 > $OUT/${lib%.so}_$rep.log 2>&1 || { echo "prof $lib $rep failed"; exit 1; }
 done; done
 python - $OUT <<'PY'
 import csv, glob, sys

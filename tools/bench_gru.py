@@ -79,10 +79,10 @@ def main():
     ap.add_argument("--H", type=int, default=512)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--variants", default="xc:0,seq:0",
-                    help="kind:dbg[:depth]; kind xc (column-split, forced), xcs (write-through exchange), "
+                    help="kind:dbg[:depth[:skew]]; kind xc (column-split, forced), xcs (write-through exchange), "
                          "xcx (members dealt over XCDs), seq (row-owning), step (per-step)")
-    ap.add_argument("--bwd-variants", default="P:0:2", help="rows:dbg:streams; rows P (row-owning), S (128x128 "
-                    "per-step, `streams` chains), 128 / 64 (per-step 256x256 / 128-row tiles)")
+    ap.add_argument("--bwd-variants", default="P:0:2", help="rows:dbg:streams[:skew]; rows P (row-owning), S (128x128 "
+                    "per-step, `streams` chains), 128 / 64 (per-step 256x256 / 128-row tiles); skew: option gru_bwd_skew")
     a = ap.parse_args()
     dev = torch.device("cuda")
     recs, keep = setup(a.B, a.T, a.H, dev)
@@ -94,7 +94,9 @@ def main():
     for v in a.bwd_variants.split(","):
         if not v:
             continue
-        rows, dbg, strm = (v.split(":") + ["0", "2"])[:3]
+        p = v.split(":")
+        rows, dbg, strm, skew = p[0], (p + ["0"])[1], (p + ["0", "2"])[2], (p + ["0", "2", "0"])[3]
+        set_option("gru_bwd_skew", int(skew))
         set_option("gru_bwd_persist", 1 if rows == "P" else 0)
         set_option("gru_bwd_big", 0 if rows == "S" else 1)
         set_option("gru_bwd_rows", 128 if rows in ("P", "S") else int(rows))
@@ -116,7 +118,9 @@ def main():
     for v in a.variants.split(","):
         if not v:
             continue
-        kind, dbg, *depth = v.split(":")
+        kind, dbg, *rest = v.split(":")
+        depth = rest[:1]
+        set_option("gru_fwd_skew", int(rest[1]) if len(rest) > 1 else 0)
         set_option("gru_step", 1 if kind == "step" else 0)
         os.environ["TT_GRU_DBG"] = dbg  # read only by a -DTT_DIAG build
         set_option("gru_depth", int(depth[0]) if depth else 4)

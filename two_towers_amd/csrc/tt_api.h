@@ -33,6 +33,8 @@ enum Opt {
                         // applies (+4: write-through exchange images; +16: members dealt across XCDs)
   OPT_GRU_XC_SKIP,      // diagnostic: member m-1 of group 0 never publishes (0: off); the others' waits time out
   OPT_GRU_XC_SPINS,     // column-split wait bound: log2 of the poll count before a wait gives up (default 22)
+  OPT_GRU_BWD_SKEW,     // gru_bwd_rows: start delay (s_sleep 127 units) of half the workgroups of each XCD
+  OPT_GRU_FWD_SKEW,     // gru_fwd_xcp: start delay (s_sleep 127 units) of the odd groups
   OPT_N
 };
 int opt(Opt o);

@@ -45,6 +45,7 @@ struct BwdArgs {
   int B, T, H;
   long ldy, ldd, ldf;
   int s;
+  int skew;  // gru_bwd_rows: odd workgroups of an XCD start skew x s_sleep(127) late (option gru_bwd_skew)
 #ifdef TT_DIAG
   int dbg;  // diagnostic build only: 1 no GEMM, 2 no epilogue loads, 4 no stores
 #endif
@@ -598,6 +599,10 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
   const bf16_t* W = static_cast<const bf16_t*>(R.whh);
   const uint32_t lbase = __builtin_amdgcn_readfirstlane(ttg::lds_addr_of(lds));
   constexpr int NK = 3 * H / 32;  // 32-deep K-tiles per step
+  // workgroups in lockstep put every CU in its product phase (L2-bound) at the same time and
+  // then in its HBM-bound epilogue; a start skew for half of them interleaves the phases
+  if (a.skew > 0 && ((blockIdx.x >> 3) & 1))
+    for (int i = 0; i < a.skew; ++i) __builtin_amdgcn_s_sleep(127);
   const long ldr = (long)T_ * a.ldd;
   // DMA pieces of a slot, wave + 8j (j < P): piece 0..7 = the A image (row q >> 2, chunk
   // slot q & 3 of 16-byte unit q), then NQ x 8 pieces of W_hh sub-images (k-row q >> 4,
@@ -1185,6 +1190,7 @@ struct XcWs {
   int rpg;        // batch rows per group
   int nround;     // rounds of RR rows per group
   int fast_ok;    // the exchange may stay in the XCD's L2 where the group shares one
+  int skew;       // odd groups start skew x s_sleep(127) late (option gru_fwd_skew; speed only)
 };
 
 TT_DEV void xc_wait(xc_gu32* cnt, unsigned target, const XcWs& ws) {
@@ -1354,6 +1360,9 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
   bf16_t* X1 = static_cast<bf16_t*>(R.x1);
   bf16_t* S = static_cast<bf16_t*>(R.save);
   const bool fast = xc_group_on_one_xcd(ws.cnt + grp * xc::CSTR, M, mem, ws.fast_ok != 0, ws);
+  // every member of a group is delayed alike (they wait for each other at every step)
+  if (ws.skew > 0 && (grp & 1))
+    for (int i = 0; i < ws.skew; ++i) __builtin_amdgcn_s_sleep(127);
   const int NS = ws.nround * T_;  // steps over all rounds
   // step idx -> its step in the round, time, first batch row, rows
   struct Step {
@@ -1681,6 +1690,7 @@ static bool xc_geometry(const XcDev& dev, int dtype, int H, int nrec, int B, int
   g.w.fast_ok = (v & 4) ? 0 : 1;  // option bit 4: always write-through images
   g.w.xmap = (v & 16) ? 1 : 0;    // option bit 16: members dealt over the XCDs
   g.w.skip = tt::opt(tt::OPT_GRU_XC_SKIP);
+  g.w.skew = tt::opt(tt::OPT_GRU_FWD_SKEW);
   const int sp = std::min(30, std::max(10, tt::opt(tt::OPT_GRU_XC_SPINS)));
   g.w.spins = 1u << sp;
   g.grid = ng * M;
@@ -1841,6 +1851,7 @@ extern "C" int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B
     TT_CHECK_HIP(hipMemsetAsync(r.dbias_part, 0, sizeof(float) * 4L * H * tt_gru_bias_rows(B), st));
   }
   a.B = B; a.T = T; a.H = H; a.ldy = ldy; a.ldd = ldd; a.ldf = ldf;
+  a.skew = tt::opt(tt::OPT_GRU_BWD_SKEW);
 #ifdef TT_DIAG
   if (const char* e = getenv("TT_GRU_DBG")) a.dbg = atoi(e);
 #endif

@@ -29,6 +29,14 @@
 
 namespace {
 
+// Timing-only diagnostic switches (`make exp EXP=-DHN_DIAG=n`; results are wrong):
+// 1 no tile DMAs after the first two, 2 no MFMAs, 4 no chunk-max epilogue, 8 no query loads
+#ifndef HN_DIAG
+#define HN_DIAG 0
+#endif
+#ifndef HN_PAIR_PREFETCH
+#define HN_PAIR_PREFETCH 1
+#endif
 constexpr int SC_COLS = 64;     // document columns per tile (= per chunk)
 constexpr int SC_RB = 2;        // 16-query MFMA blocks per wave
 constexpr int SC_TPS_MAX = 32;  // tiles per workgroup (chunk-max staging)
@@ -44,6 +52,20 @@ struct ScanCfg {
   static constexpr int SLOTS = KS <= 8 ? 4 : 2;
 };
 
+// max of three scores in one v_max3_f32: fmaxf() would also quiet each input (an extra
+// v_max_f32 x, x per operand under the IEEE mode); the scores are finite
+TT_DEV float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+// max of the 16 scores a lane holds for one query in a 64-document tile
+TT_DEV float max16(const float (&v)[16]) {
+  float m = vmax3(v[0], v[1], v[2]);
+#pragma unroll
+  for (int j = 3; j < 15; j += 2) m = vmax3(m, v[j], v[j + 1]);
+  return vmax3(m, v[15], v[15]);
+}
 // max over the four 16-lane rows of a wave (lanes l, l+16, l+32, l+48), result in all
 TT_DEV float rowgroup_max4(float v) {
   const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
@@ -138,7 +160,8 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
 #pragma unroll
   for (int qb = 0; qb < SC_RB; ++qb)
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) qa[qb][ks] = ld_frag(Q, row0 + qb * 16 + (lane & 15), bq, h, ks);
+    for (int ks = 0; ks < KS; ++ks)
+      qa[qb][ks] = (HN_DIAG & 8) ? make_uint4(lane, ks, qb, 1) : ld_frag(Q, row0 + qb * 16 + (lane & 15), bq, h, ks);
   // Retire the query loads here, so that hipcc does not place a vmcnt(0) inside the tile
   // loop (it cannot see the LDS-DMAs and would wait for the tiles in flight every tile).
 #pragma unroll
@@ -153,6 +176,11 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
   // With two slots (h 512) every tile is retired alone and the next one requested into
   // the slot its predecessor freed.
   auto sync = [&](int t) {
+    if (HN_DIAG & 1) {
+      if (t == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if ((t & 1) == 0) __builtin_amdgcn_s_barrier();
+      return;
+    }
     if (SC_SLOTS == 2) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -166,6 +194,7 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
   };
   // Chunk maxima of tile t (masked form: positive -> -1, documents past nd -> -inf).
   auto chunk_max = [&](const f32x4 (&a)[4][SC_RB], int t, bool masked) {
+    if (HN_DIAG & 4) return;
     const int n0 = (int)((t0 + t) * SC_COLS);
     const bool diag = label_off >= 0 && label_off + row0 < n0 + SC_COLS && n0 < label_off + row0 + SC_RB * 16;
 #pragma unroll
@@ -187,10 +216,7 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
             if (doc >= lim) v[db * 4 + r] = -FLT_MAX;
           }
       }
-      float m = fmaxf(fmaxf(v[0], v[1]), v[2]);
-#pragma unroll
-      for (int j = 3; j < 15; j += 2) m = fmaxf(fmaxf(m, v[j]), v[j + 1]);
-      m = rowgroup_max4(fmaxf(m, v[15]));
+      const float m = rowgroup_max4(max16(v));
       if (lane < 16) cms[t * SC_ROWS + wave * SC_RB * 16 + qb * 16 + lane] = m;
     }
   };
@@ -199,18 +225,29 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
   // the fragment reads of k-step ks+2, the 8 MFMAs of ks, then one slice of the epilogue,
   // so the LDS reads run two k-steps ahead and the epilogue VALU fills MFMA issue gaps
   // (hipcc otherwise sinks every read to just before its MFMA and clusters the VALU).
-  auto tile = [&](f32x4 (&acc)[4][SC_RB], const f32x4 (&prev)[4][SC_RB], int t, bool epi) {
+  // fragment ring: k-step ks of a tile in fa[(ks + OFF) % 3]. PRE_IN: k-steps 0, 1 were
+  // requested by the previous tile (the first of a pair, both in LDS since the pair's
+  // barrier), PRE_OUT: request the next tile's first two k-steps during the last two.
+  uint4 fa[3][4];
+  auto frag_of = [&](const char* img, int ks, int db) {
+    return *reinterpret_cast<const uint4*>(img + TI::off(db * 16 + (lane & 15), ks * 4 + (lane >> 4)));
+  };
+  auto tile = [&](f32x4 (&acc)[4][SC_RB], const f32x4 (&prev)[4][SC_RB], int t, bool epi, auto pre_in,
+                  auto pre_out) {
+    constexpr int OFF = decltype(pre_in)::value ? KS % 3 : 0;
+    constexpr bool PRE_OUT = decltype(pre_out)::value;
     const char* img = lds + (t % SC_SLOTS) * TI::BYTES;
+    const char* nimg = lds + ((t + 1) % SC_SLOTS) * TI::BYTES;
 #pragma unroll
     for (int db = 0; db < 4; ++db)
 #pragma unroll
       for (int qb = 0; qb < SC_RB; ++qb) acc[db][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    uint4 fa[3][4];
+    if constexpr (!decltype(pre_in)::value) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int db = 0; db < 4; ++db)
-        fa[ks][db] = *reinterpret_cast<const uint4*>(img + TI::off(db * 16 + (lane & 15), ks * 4 + (lane >> 4)));
+        for (int db = 0; db < 4; ++db) fa[(ks + OFF) % 3][db] = frag_of(img, ks, db);
+    }
     // epilogue slice i: query block i / 3; two half-maxima (documents 0-31, 32-63), then
     // the 4-row-group reduction and the store
     float m = 0.f;
@@ -219,9 +256,8 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
       if (qb >= SC_RB) return;
       if (part < 2) {
         const f32x4 x = prev[2 * part][qb], y = prev[2 * part + 1][qb];
-        const float hm =
-            fmaxf(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])), fmaxf(fmaxf(y[0], y[1]), fmaxf(y[2], y[3])));
-        m = part == 0 ? hm : fmaxf(m, hm);
+        const float hm = vmax3(vmax3(x[0], x[1], x[2]), vmax3(x[3], y[0], y[1]), vmax3(y[2], y[3], y[3]));
+        m = part == 0 ? hm : vmax3(m, hm, hm);
       } else {
         m = rowgroup_max4(m);
         if (lane < 16) cms[(t - 1) * SC_ROWS + wave * SC_RB * 16 + qb * 16 + lane] = m;
@@ -232,19 +268,24 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
     for (int ks = 0; ks < KS; ++ks) {
       if (ks + 2 < KS) {
 #pragma unroll
-        for (int db = 0; db < 4; ++db)
-          fa[(ks + 2) % 3][db] =
-              *reinterpret_cast<const uint4*>(img + TI::off(db * 16 + (lane & 15), (ks + 2) * 4 + (lane >> 4)));
+        for (int db = 0; db < 4; ++db) fa[(ks + 2 + OFF) % 3][db] = frag_of(img, ks + 2, db);
+      } else if (PRE_OUT) {
+#pragma unroll
+        for (int db = 0; db < 4; ++db) fa[(ks + 2 + OFF) % 3][db] = frag_of(nimg, ks + 2 - KS, db);
       }
 #pragma unroll
       for (int db = 0; db < 4; ++db)
 #pragma unroll
-        for (int qb = 0; qb < SC_RB; ++qb)
-          acc[db][qb] = ttg::mma<bf16_t>(fa[ks % 3][db], qa[qb][ks], acc[db][qb]);
-      if (epi) slice(ks);
+        for (int qb = 0; qb < SC_RB; ++qb) {
+          if (HN_DIAG & 2)
+            asm volatile("" ::"v"(fa[(ks + OFF) % 3][db].x), "v"(qa[qb][ks].x));
+          else
+            acc[db][qb] = ttg::mma<bf16_t>(fa[(ks + OFF) % 3][db], qa[qb][ks], acc[db][qb]);
+        }
+      if (epi && !(HN_DIAG & 4)) slice(ks);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (epi) {
+    if (epi && !(HN_DIAG & 4)) {
 #pragma unroll
       for (int i = KS; i < 3 * SC_RB; ++i) slice(i);
     }
@@ -256,24 +297,29 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
     return (label_off >= 0 && label_off + row0 < n0 + SC_COLS && n0 < label_off + row0 + SC_RB * 16) ||
            n0 + SC_COLS > nd;
   };
-  auto step = [&](f32x4 (&cur)[4][SC_RB], const f32x4 (&prev)[4][SC_RB], int t) {  // t >= 1
+  // pairs of tiles (4-slot ring): the first of a pair hands the second its first fragments
+  using pre_t = std::bool_constant<SC_SLOTS == 4 && HN_PAIR_PREFETCH>;
+  using no_t = std::false_type;
+  auto step = [&](f32x4 (&cur)[4][SC_RB], const f32x4 (&prev)[4][SC_RB], int t, auto pre_in, auto pre_out) {
     sync(t);
     if (special(t - 1)) {
-      tile(cur, prev, t, false);
+      tile(cur, prev, t, false, pre_in, pre_out);
       chunk_max(prev, t - 1, true);
     } else {
-      tile(cur, prev, t, true);
+      tile(cur, prev, t, true, pre_in, pre_out);
     }
   };
   sync(0);
-  tile(accB, accA, 0, false);
+  if (nt > 1) tile(accB, accA, 0, false, no_t{}, pre_t{});
+  else tile(accB, accA, 0, false, no_t{}, no_t{});
   int t = 1;
   for (; t + 1 < nt; t += 2) {
-    step(accA, accB, t);
-    step(accB, accA, t + 1);
+    step(accA, accB, t, pre_t{}, no_t{});                 // second of a pair
+    if (t + 2 < nt) step(accB, accA, t + 1, no_t{}, pre_t{});  // first of the next pair
+    else step(accB, accA, t + 1, no_t{}, no_t{});
   }
   if (t < nt) {
-    step(accA, accB, t);
+    step(accA, accB, t, pre_t{}, no_t{});
     chunk_max(accA, t, special(t));
   } else {
     chunk_max(accB, t - 1, special(t - 1));

@@ -225,6 +225,10 @@ def main():
         return
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         raise SystemExit(spawn_local_ranks(args.gpus))
+    # stdout carries exactly the one JSON line: anything the runtime libraries print to it
+    # (RCCL's version banner at communicator creation) goes to stderr instead
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -235,7 +239,10 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     group = None
-    if world > 1:
+    # TT_DIST_FORCE=1 under a launcher: a one-rank group whose collectives still run (RCCL
+    # rehearsal of the DP path on one GPU)
+    forced = os.environ.get("TT_DIST_FORCE", "0") == "1" and "WORLD_SIZE" in os.environ
+    if world > 1 or forced:
         if backend == "nccl":
             tdist.init_process_group("nccl", device_id=dev)
         else:
@@ -368,15 +375,17 @@ def main():
                     f"10% pad tail per row, random-init weights (torch seed 1234)",
             "config": {"workload": workload_name(args, world),
                        "global_batch": B * world, "seq_len": T, "hidden": h, "embedding_dim": E,
-                       "parallelism": f"dp{world}", "loss": args.loss},
+                       "parallelism": f"dp{world}", "loss": args.loss,
+                       "collectives": (("rccl" if backend == "nccl" else backend) + (" (forced at one rank)" if forced else ""))
+                       if tdist.is_initialized() else None},
             "roofline": roofline,
             "rooflines_secondary": extra,
             "kernel_ms_per_step": kernels,
             "loss_first_last": [round(first_loss, 5), round(final_loss, 5)],
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line))
-    if world > 1:
+        print(json.dumps(line), file=out, flush=True)
+    if tdist.is_initialized():
         tdist.destroy_process_group()
 
 

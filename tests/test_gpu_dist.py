@@ -115,13 +115,19 @@ def _dp_model(z):
     return m.cuda().eval()
 
 
-def _step_rank(rank, world, port, kind, overlap, out):
+def _step_rank(rank, world, port, kind, overlap, out, backend="gloo"):
     """train_enhanced.py:58-63 on this rank's rows: zero_grad, forward, loss (global
     negative pool), backward, gradient all-reduce, Adam. overlap: the tower gradients are
     summed inside the backward (set_process_group(..., overlap_grad_allreduce=True)) and
-    allreduce_grads sums only the rest; otherwise allreduce_grads sums everything."""
+    allreduce_grads sums only the rest; otherwise allreduce_grads sums everything.
+    backend "nccl" (RCCL) with world 1: TT_DIST_FORCE=1 makes every collective run anyway."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        os.environ["TT_DIST_FORCE"] = "1"
+        torch.cuda.set_device(0)
+        torch.distributed.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import two_towers_amd as tta
         from two_towers_amd import dist as tdp
@@ -183,6 +189,33 @@ def test_dp_train_step_matches_reference_global_batch(kind, world, overlap):
             assert float(np.abs(w - z[f"{kind}.w1.{k}"]).max()) <= 1e-5, (r, k)
         if idx is not None:
             assert (idx == z["hardneg.idx"][r * n:(r + 1) * n]).all()
+
+
+@pytest.mark.parametrize("kind", ["infonce", "hardneg"])
+def test_rccl_one_rank_train_step_matches_reference(kind):
+    """The DP step's collectives over RCCL ("nccl") on the box's one GPU: a one-rank process
+    group with TT_DIST_FORCE=1, so the doc-vector all-gather, its reduce-scatter, the loss
+    all-reduce and the overlapped + bucketed gradient all-reduces all execute as RCCL
+    kernels (the 8-GPU node runs the same calls). Must reproduce the reference's
+    single-process step on dp_step.npz exactly as the gloo worlds do."""
+    import numpy as np
+    z = _dp_golden()
+    ctx = mp.get_context("spawn")
+    out = ctx.Queue()
+    p = ctx.Process(target=_step_rank, args=(0, 1, _port(), kind, True, out, "nccl"))
+    p.start()
+    _, loss, grads, w1, idx = out.get(timeout=180)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    ref = float(z[f"{kind}.loss"])
+    assert abs(loss - ref) <= 1e-5 * abs(ref), (loss, ref)
+    for k, g in grads.items():
+        gr = z[f"{kind}.g.{k}"]
+        assert float(np.abs(g - gr).max()) <= 2e-3 * float(np.abs(gr).max()) + 1e-9, k
+    for k, w in w1.items():
+        assert float(np.abs(w - z[f"{kind}.w1.{k}"]).max()) <= 1e-5, k
+    if idx is not None:
+        assert (idx == z["hardneg.idx"]).all()
 
 
 def _drop_rank(rank, world, port, out):

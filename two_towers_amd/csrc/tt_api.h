@@ -34,6 +34,7 @@ enum Opt {
   OPT_GRU_XC_SKIP,      // diagnostic: member m-1 of group 0 never publishes (0: off); the others' waits time out
   OPT_GRU_XC_SPINS,     // column-split wait bound: log2 of the poll count before a wait gives up (default 22)
   OPT_GRU_BWD_SKEW,     // gru_bwd_rows: start delay (s_sleep 127 units) of half the workgroups of each XCD
+                        // (default 14, about half a step at configs[2]: 7.05-7.09 vs 7.49-7.54 ms per launch)
   OPT_GRU_FWD_SKEW,     // gru_fwd_xcp: start delay (s_sleep 127 units) of the odd groups
   OPT_N
 };

@@ -36,7 +36,7 @@ constexpr OptDef kOpts[OPT_N] = {
     {"infonce_flash", "TT_INFONCE_FLASH", 1},     {"hn_map", "TT_HN_MAP", 0},
     {"gemm_skew", "TT_GEMM_SKEW", 0},             {"gemm_persist_maxk", "TT_GEMM_PERSIST_MAXK", 24},
     {"gru_fwd_xc", "TT_GRU_FWD_XC", 1},           {"gru_xc_skip", "TT_GRU_XC_SKIP", 0},
-    {"gru_xc_spins", "TT_GRU_XC_SPINS", 22},      {"gru_bwd_skew", "TT_GRU_BWD_SKEW", 0},
+    {"gru_xc_spins", "TT_GRU_XC_SPINS", 22},      {"gru_bwd_skew", "TT_GRU_BWD_SKEW", 14},
     {"gru_fwd_skew", "TT_GRU_FWD_SKEW", 0},
 };
 struct OptTable {

@@ -10,12 +10,23 @@ so the summed gradients are exactly the single-process gradients of the whole ba
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
 
+def forced() -> bool:
+    """TT_DIST_FORCE=1: run every collective even in a one-rank process group, so the DP
+    path's RCCL calls (all-gather, reduce-scatter, bucketed and overlapped all-reduce)
+    execute on a single GPU (tests/test_gpu_dist.py, bench.py rehearsal)."""
+    return os.environ.get("TT_DIST_FORCE", "0") == "1"
+
+
 def active(group=None) -> bool:
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return dist.get_world_size(group) > 1 or forced()
 
 
 def rank_world(group=None):
@@ -26,9 +37,9 @@ def rank_world(group=None):
 
 def all_gather_rows(x: torch.Tensor, group=None) -> torch.Tensor:
     """[B_l, ...] on every rank -> [world * B_l, ...] in rank order (no autograd)."""
-    r, w = rank_world(group)
-    if w == 1:
+    if not active(group):
         return x
+    r, w = rank_world(group)
     out = torch.empty((w * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     dist.all_gather_into_tensor(out, x.contiguous(), group=group)
     return out
@@ -36,9 +47,9 @@ def all_gather_rows(x: torch.Tensor, group=None) -> torch.Tensor:
 
 def reduce_scatter_rows(x: torch.Tensor, group=None) -> torch.Tensor:
     """[world * B_l, ...] partial sums on every rank -> this rank's [B_l, ...] total."""
-    r, w = rank_world(group)
-    if w == 1:
+    if not active(group):
         return x
+    r, w = rank_world(group)
     out = torch.empty((x.shape[0] // w,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     dist.reduce_scatter_tensor(out, x.contiguous(), op=dist.ReduceOp.SUM, group=group)
     return out

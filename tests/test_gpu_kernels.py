@@ -225,3 +225,36 @@ def test_gemm_persistent_bf16_output_is_rounded_fp32(stream):
     assert rel_err(got[kept] / (1 / 0.9), ref[kept]) < 1e-5
     frac = 1 - float(kept.float().mean())
     assert 0.08 < frac < 0.12, frac
+
+
+@pytest.mark.parametrize("m,n,k,nb,with_bias", [(524288, 3072, 320, 2, True), (70000, 3072, 320, 2, True),
+                                                (65579, 1536, 96, 1, False), (40000, 384, 352, 2, True)])
+def test_gemm_b_resident_matches_persistent(m, n, k, nb, with_bias):
+    """gemm_bres (the layer-0 input projection: each workgroup keeps a 192-column panel of
+    B in LDS, its waves walk 32-row A tiles with no barrier) against the persistent 256x256
+    kernel (option gemm_bres = 0) on the same operands: the same MFMA instruction, operand
+    roles and k order, so every bf16 output must be identical. The bench shape (M = B*T
+    = 524,288, N = 6H = 3072, K = Ep = 320, two towers) and shapes whose rows do not fill
+    the 32-row tiles of the 8 row groups, with and without bias, K 96 and 352 (a partial
+    64-deep K-tile image)."""
+    from two_towers_amd._lib import option
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(m + n + k)
+    A = [torch.randn(m, k, generator=g, device=DEV).to(dt) for _ in range(nb)]
+    B = [(torch.randn(n, k, generator=g, device=DEV) * k ** -0.5).to(dt) for _ in range(nb)]
+    bias = [torch.randn(n, generator=g, device=DEV) for _ in range(nb)] if with_bias else None
+    outs = []
+    for br in (1, 0):
+        C = [torch.full((m, n), float("nan"), device=DEV, dtype=dt) for _ in range(nb)]
+        with option("gemm_bres", br):
+            ops.gemm(A, B, C, m=m, n=n, k=k, lda=k, ldb=k, ldc=n, a_kouter=False, b_kouter=False, dtype=dt,
+                     out_dtype=dt, bias=bias, splits=1)
+        torch.cuda.synchronize()
+        outs.append(C)
+    for i in range(nb):
+        bad = int((outs[0][i].view(torch.int16) != outs[1][i].view(torch.int16)).sum())
+        assert bad == 0, f"batch {i}: {bad} of {m * n} outputs differ"
+    # and against fp32 math on a sample of rows
+    rows = torch.randint(0, m, (512,), generator=g, device=DEV)
+    ref = A[0][rows].float() @ B[0].float().t() + (bias[0] if with_bias else 0)
+    assert rel_err(outs[0][0][rows].float(), ref) < 8e-3

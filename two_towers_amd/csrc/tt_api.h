@@ -36,6 +36,7 @@ enum Opt {
   OPT_GRU_BWD_SKEW,     // gru_bwd_rows: start delay (s_sleep 127 units) of half the workgroups of each XCD
                         // (default 14, about half a step at configs[2]: 7.05-7.09 vs 7.49-7.54 ms per launch)
   OPT_GRU_FWD_SKEW,     // gru_fwd_xcp: start delay (s_sleep 127 units) of the odd groups
+  OPT_GEMM_BRES,        // 0: no B-resident short-K GEMM (layer-0 input projection)
   OPT_N
 };
 int opt(Opt o);

@@ -37,7 +37,7 @@ constexpr OptDef kOpts[OPT_N] = {
     {"gemm_skew", "TT_GEMM_SKEW", 0},             {"gemm_persist_maxk", "TT_GEMM_PERSIST_MAXK", 24},
     {"gru_fwd_xc", "TT_GRU_FWD_XC", 1},           {"gru_xc_skip", "TT_GRU_XC_SKIP", 0},
     {"gru_xc_spins", "TT_GRU_XC_SPINS", 22},      {"gru_bwd_skew", "TT_GRU_BWD_SKEW", 14},
-    {"gru_fwd_skew", "TT_GRU_FWD_SKEW", 0},
+    {"gru_fwd_skew", "TT_GRU_FWD_SKEW", 0},       {"gemm_bres", "TT_GEMM_BRES", 1},
 };
 struct OptTable {
   std::atomic<int> v[OPT_N];
@@ -376,6 +376,126 @@ TT_DEV void epi_direct(const GemmArgs& g, const f32x4 (&acc)[8][4], TO* C, const
           else
             for (int e = 0; e < 4 && c + e < g.N; ++e) Elt<TO>::st(C + (long)gm * g.ldc + c + e, v[e]);
         }
+      }
+    }
+  }
+}
+
+// ---- B-resident short-K GEMM (the GRU's layer-0 input projection) ----------------------
+// C_b[m][n] = A_b[m][:K] . B_b[n][:K] + bias_b[n], bf16 in and out, fp32 accumulation,
+// K <= 384 and a multiple of 32, N a multiple of 192 (input_proj_l0: M = B*T, N = 6H =
+// 3072, K = Ep = 320). The persistent 256x256 GEMM spends most of such a tile outside
+// the MFMAs -- 5 K-tiles of products, then an epilogue whose 128 KiB of stores do not
+// overlap them -- because all 8 waves of a tile meet at every barrier.
+// Here each workgroup keeps one 192-column panel of B (K x 192 bf16, <= 144 KiB) in LDS
+// for the whole launch, and its 8 waves walk 32-row A tiles INDEPENDENTLY: A fragments
+// come straight from global memory (16 bytes per lane, NKS/2 k-steps ahead, across tile
+// boundaries), so the main loop has no barrier at all and one wave's epilogue stores run
+// beside the other waves' MFMAs. The 8 XCD-local groups of workgroups (one per M range)
+// cover all panels, so each A row is fetched into an XCD's L2 once and read by the 16
+// (or 32) panels' workgroups. Same MFMA (16x16x32, B fragment first: the transposed
+// accumulate of the persistent kernel), same k order from zero: bit-identical to it.
+constexpr int BR_COLS = 192;  // B panel columns per workgroup
+template <int NKS>  // k-steps of 32
+__global__ __launch_bounds__(512, 1) void gemm_bres(GemmArgs g, int npan, int nbatch) {
+  constexpr int NKT = (NKS + 1) / 2;  // 64-deep K-tile images
+  constexpr int IMG = BR_COLS * ttg::KTB;
+  constexpr int PD = NKS % 2 == 0 ? NKS / 2 : NKS;  // A prefetch depth in k-steps (divides NKS)
+  __shared__ __attribute__((aligned(16))) char lds[NKT * IMG + BR_COLS * 4];
+  float* bias_s = reinterpret_cast<float*>(lds + NKT * IMG);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // workgroup -> (row group gi, batch entry bi, panel): consecutive ids (one XCD's run)
+  // share a row group, so its A rows are read into that L2 once for all panels
+  const int ptot = npan * nbatch;
+  const int bid = ttg::xcd_remap(blockIdx.x, gridDim.x);
+  const int ngrp = gridDim.x / ptot;
+  const int gi = bid / ptot, p = bid % ptot;
+  const int bi = p / npan, n0 = (p % npan) * BR_COLS;
+  const bf16_t* A = static_cast<const bf16_t*>(g.a[bi]);
+  const bf16_t* Bm = static_cast<const bf16_t*>(g.b[bi]);
+  bf16_t* C = static_cast<bf16_t*>(g.c[bi]);
+  const float* bias = g.bias[bi];
+  // the panel of B -> K-tile images (rows of 128 B, kc_off swizzle), zero past K; bias -> LDS
+  for (int id = tid; id < NKT * BR_COLS * 8; id += 512) {
+    const int kt = id / (BR_COLS * 8), rem = id % (BR_COLS * 8), row = rem >> 3, c = rem & 7;
+    const int k = kt * 64 + c * 8;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (k < g.K) v = *reinterpret_cast<const uint4*>(Bm + (long)(n0 + row) * g.ldb + k);
+    *reinterpret_cast<uint4*>(lds + kt * IMG + ttg::kc_off(row, c)) = v;
+  }
+  for (int c = tid; c < BR_COLS; c += 512) bias_s[c] = bias ? bias[n0 + c] : 0.f;
+  __syncthreads();
+  // this group's rows, in 32-row tiles dealt to the waves round-robin
+  const int mg = ((g.M + ngrp - 1) / ngrp + 31) / 32 * 32;
+  const int g0 = gi * mg;
+  const int ntl = max(0, min(mg, g.M - g0) + 31) / 32;
+  const __amdgpu_buffer_rsrc_t ra = tt_rsrc_n(A + (long)g0 * g.lda, g0 < g.M);
+  const int lr = lane & 15, q = lane >> 4;
+  // A fragment of (tile t, k-step ks, row block rb): rows past M read zero (offset past the
+  // resource's range)
+  auto lda_frag = [&](int t, int ks, int rb) {
+    const int row = t * 32 + rb * 16 + lr;
+    const uint32_t off = t < ntl && g0 + row < g.M ? (uint32_t)((row * (int)g.lda + ks * 32 + q * 8) * 2) : 0x80000000u;
+    return ld16_buf(ra, off, 0);
+  };
+  uint4 ar[PD][2];
+  int t = wave;
+#pragma unroll
+  for (int i = 0; i < PD; ++i) {
+    ar[i][0] = lda_frag(t, i, 0);
+    ar[i][1] = lda_frag(t, i, 1);
+  }
+  for (; t < ntl; t += 8) {
+    f32x4 acc[2][BR_COLS / 16];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int j = 0; j < BR_COLS / 16; ++j) acc[rb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const uint4 a0 = ar[ks % PD][0], a1 = ar[ks % PD][1];
+      // refill the slot: k-step ks + PD of this tile, or of the wave's next tile
+      if (ks + PD < NKS) {
+        ar[ks % PD][0] = lda_frag(t, ks + PD, 0);
+        ar[ks % PD][1] = lda_frag(t, ks + PD, 1);
+      } else {
+        ar[ks % PD][0] = lda_frag(t + 8, ks + PD - NKS, 0);
+        ar[ks % PD][1] = lda_frag(t + 8, ks + PD - NKS, 1);
+      }
+      const char* img = lds + (ks >> 1) * IMG;
+#pragma unroll
+      for (int j = 0; j < BR_COLS / 16; ++j) {
+        const uint4 fb = ttg::frag<bf16_t, false>(img, 16 * j, ks & 1);
+        acc[0][j] = ttg::mma<bf16_t>(fb, a0, acc[0][j]);
+        acc[1][j] = ttg::mma<bf16_t>(fb, a1, acc[1][j]);
+      }
+      // one k-step per scheduling region: hipcc would otherwise hoist every B fragment
+      // read of the tile ahead of the MFMAs (and spill)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // epilogue: acc[rb][j][e] = C(row 32t + 16rb + lr, col 16j + 4q + e); bias, bf16, pairs of
+    // column tiles exchanged (v_permlane16_swap) into 16-byte row stores
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int row = t * 32 + rb * 16 + lr;
+      const bool ok = g0 + row < g.M;
+#pragma unroll
+      for (int jp = 0; jp < BR_COLS / 32; ++jp) {
+        uint32_t w[2][2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int j = 2 * jp + h;
+          const float4 b4 = *reinterpret_cast<const float4*>(bias_s + 16 * j + 4 * q);
+          const float v0 = acc[rb][j][0] + b4.x, v1 = acc[rb][j][1] + b4.y;
+          const float v2 = acc[rb][j][2] + b4.z, v3 = acc[rb][j][3] + b4.w;
+          w[h][0] = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+          w[h][1] = (uint32_t)f2bf(v2) | ((uint32_t)f2bf(v3) << 16);
+        }
+        const auto s0 = __builtin_amdgcn_permlane16_swap(w[0][0], w[1][0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(w[0][1], w[1][1], false, false);
+        const int cs = n0 + 16 * (2 * jp + (q & 1)) + 8 * (q >> 1);
+        if (ok)
+          *reinterpret_cast<uint4*>(C + (long)(g0 + row) * g.ldc + cs) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
       }
     }
   }
@@ -750,9 +870,45 @@ int launch_persist(int akout, int bkout, bool shift, const GemmArgs& g, int ntil
   return 0;
 }
 
+// gemm_bres where it applies (bf16 NT, bias only, N % 192 == 0, short K): returns true if launched
+template <typename T, typename TO>
+bool try_bres(int akout, int bkout, bool shift, const GemmArgs& g, int nbatch, hipStream_t st, int* rc) {
+  *rc = 0;
+  if constexpr (!std::is_same<T, bf16_t>::value || !std::is_same<TO, bf16_t>::value) {
+    return false;
+  } else {
+    if (tt::opt(tt::OPT_GEMM_BRES) == 0 || akout || bkout || shift || g.splits != 1 || g.beta || g.relu ||
+        g.drop_thresh || g.alpha != 1.f || g.force_regstage)
+      return false;
+    if (g.N % BR_COLS || g.K % 32 || g.K < 32 || g.K > 384 || !g.vec_ok || (g.lda * 2) % 16) return false;
+    for (int b = 0; b < nbatch; ++b)
+      if (g.bias[b] && (uintptr_t)g.bias[b] % 16) return false;
+    const int npan = g.N / BR_COLS, ptot = npan * nbatch, nwg = 256;
+    if (ptot > nwg || nwg % ptot) return false;
+    if ((long)g.M < (long)(nwg / ptot) * 256 || (long)g.M * g.lda * 2 >= (1L << 31)) return false;
+    const dim3 grid(nwg), blk(512);
+    switch (g.K / 32) {
+#define TT_BR(n) case n: hipLaunchKernelGGL(gemm_bres<n>, grid, blk, 0, st, g, npan, nbatch); break;
+      TT_BR(1) TT_BR(2) TT_BR(3) TT_BR(4) TT_BR(5) TT_BR(6) TT_BR(7) TT_BR(8) TT_BR(9) TT_BR(10) TT_BR(11) TT_BR(12)
+#undef TT_BR
+      default: return false;
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      tt::set_error("gemm_bres: %s", hipGetErrorString(e));
+      *rc = (int)e;
+    }
+    return true;
+  }
+}
+
 template <typename T, typename TO>
 int launch_gemm(int akout, int bkout, bool shift, GemmArgs& g, int nbatch, hipStream_t st) {
   constexpr int EPC = 16 / (int)sizeof(T);
+  {
+    int rc = 0;
+    if (try_bres<T, TO>(akout, bkout, shift, g, nbatch, st, &rc)) return rc;
+  }
   const bool dma = (akout ? g.M % EPC == 0 : g.K % EPC == 0) && (bkout ? g.N % EPC == 0 : g.K % EPC == 0) &&
                    g.force_regstage != 1;
   const long t256 = (long)tt_ceil_div(g.M, 256) * tt_ceil_div(g.N, 256) * nbatch * g.splits;

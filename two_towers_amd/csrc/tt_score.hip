@@ -38,17 +38,24 @@ namespace {
 #define HN_PAIR_PREFETCH 1
 #endif
 constexpr int SC_COLS = 64;     // document columns per tile (= per chunk)
-constexpr int SC_RB = 2;        // 16-query MFMA blocks per wave
+#ifndef HN_W4
+#define HN_W4 1
+#endif
 constexpr int SC_TPS_MAX = 32;  // tiles per workgroup (chunk-max staging)
 
 // Per width (h = 32 KS). h <= 256: 8 waves (two per SIMD, 256 query rows per workgroup)
 // and a 4-slot LDS tile ring that travels in pairs. h 512: a tile is 64 KiB and the
 // query fragments alone are 128 registers per lane, so 4 waves (one per SIMD, 512
 // registers each, 128 query rows) and a 2-slot ring, one tile per barrier.
+// h 256 (HN_W4): 4 waves (one per SIMD) of 64 query rows each: every LDS fragment read
+// feeds 4 MFMAs, half the LDS read traffic of 8 waves x 32 rows (which the diagnostics put
+// at a quarter of the scan, profiles/r04_hn_scan_diag.txt), 256 rows per workgroup as before
 template <int KS>
 struct ScanCfg {
-  static constexpr int WAVES = KS <= 8 ? 8 : 4;
-  static constexpr int ROWS = WAVES * SC_RB * 16;
+  static constexpr bool W4 = KS == 8 && HN_W4;
+  static constexpr int WAVES = KS <= 8 && !W4 ? 8 : 4;
+  static constexpr int RB = W4 ? 4 : 2;  // 16-query MFMA blocks per wave
+  static constexpr int ROWS = WAVES * RB * 16;
   static constexpr int SLOTS = KS <= 8 ? 4 : 2;
 };
 
@@ -135,6 +142,7 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
                                                                  float* __restrict__ CM, int map) {
   using TI = ScanTile<KS>;
   constexpr int SC_WAVES = ScanCfg<KS>::WAVES, SC_ROWS = ScanCfg<KS>::ROWS, SC_SLOTS = ScanCfg<KS>::SLOTS;
+  constexpr int SC_RB = ScanCfg<KS>::RB;
   // tile ring + chunk maxima [tile][row]: 4 x 32 KiB + 32 KiB (h 256) or 2 x 64 KiB + 16
   // KiB (h 512), one workgroup per CU
   __shared__ __attribute__((aligned(16))) char lds[SC_SLOTS * TI::BYTES + SC_TPS_MAX * SC_ROWS * 4];
@@ -282,12 +290,12 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
           else
             acc[db][qb] = ttg::mma<bf16_t>(fa[(ks + OFF) % 3][db], qa[qb][ks], acc[db][qb]);
         }
-      if (epi && !(HN_DIAG & 4)) slice(ks);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (epi && !(HN_DIAG & 4)) {
+      if (epi && !(HN_DIAG & 4)) {
+        constexpr int NSL = 3 * SC_RB;  // slices spread evenly over the k-steps
 #pragma unroll
-      for (int i = KS; i < 3 * SC_RB; ++i) slice(i);
+        for (int i = ks * NSL / KS; i < (ks + 1) * NSL / KS; ++i) slice(i);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
   f32x4 accA[4][SC_RB], accB[4][SC_RB];

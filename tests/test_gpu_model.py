@@ -223,10 +223,11 @@ def test_big_tile_gru_backward_matches_step_kernel(B, T):
         assert cos > 0.9999 and rel(outs[1][k], outs[0][k]) < 2e-2, (k, cos)
 
 
-@pytest.mark.parametrize("h,B,T", [(256, 130, 5), (256, 520, 3), (128, 200, 6)])
+@pytest.mark.parametrize("h,B,T", [(256, 130, 5), (256, 520, 3), (128, 200, 6), (512, 300, 4), (512, 130, 3)])
 def test_row_owning_gru_backward_matches_step_kernels(h, B, T):
     """bf16 backward through the persistent row-owning kernel (one launch per layer,
-    H 512 / 256: gru_bwd_rows, 128 rows x all H units per workgroup) vs the
+    H 1024 / 512 / 256: gru_bwd_rows, 128 rows x all H units per workgroup; H 1024 in two
+    column passes of 512 units per step) vs the
     per-step launches (option gru_bwd_persist = 0): the same arithmetic per element, so
     gradients agree to accumulation order (the recurrent GEMM's K order and the bias
     partial sums differ). B 130 / 520 / 200 give tail row tiles."""

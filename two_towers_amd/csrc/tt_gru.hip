@@ -545,18 +545,24 @@ __global__ __launch_bounds__(512) void gru_bwd_big(BwdArgs a) {
 // 7.61 vs 7.81 ms per layer at configs[2] against 64-deep K-tiles in two slots.
 //   A image: 64-byte rows, 16-byte chunk c of row r at c ^ ((r >> 1) & 3) (conflict-free
 //   for the ds_read_b128 lane groups); W_hh: the K-outer bf16 image of the first 32 k-rows.
+// H 1024 (configs[4], the reference's hidden 512): the accumulator of 128 rows x H units
+// would be 256 registers per lane, so every step runs in NP = 2 column passes of HP = 512
+// units (a pass = the product of the rows' whole dL/dgh_{s+1} with W_hh's columns of the
+// pass, then the epilogue of those units); the A operand is streamed once per pass.
 template <int H>
 struct BwdRowsCfg {
-  static constexpr int NQ = H / 128;
-  static constexpr int SLOT = 8192 + NQ * 8192;  // 40 KiB at H = 512
+  static constexpr int NP = H > 512 ? H / 512 : 1;  // column passes per step
+  static constexpr int HP = H / NP;                 // units per pass
+  static constexpr int NQ = HP / 128;
+  static constexpr int SLOT = 8192 + NQ * 8192;  // 40 KiB at HP = 512
   static constexpr int NS = 4;
   static constexpr int LDS = NS * SLOT;
   static constexpr int P = SLOT / 1024 / 8;  // DMAs per wave per K-tile
-  static constexpr int NCB = H / 64;
-  static constexpr int TPR = H / 8;
+  static constexpr int NCB = HP / 64;
+  static constexpr int TPR = HP / 8;
   static constexpr int RPI = 512 / TPR;
-  static constexpr int LDB = H + 8;
-  static_assert(SLOT % 8192 == 0 && 128 * LDB * 2 <= LDS && RPI * 4 * H * 4 <= LDS, "ring layout");
+  static constexpr int LDB = HP + 8;
+  static_assert(SLOT % 8192 == 0 && 128 * LDB * 2 <= LDS && RPI * 4 * HP * 4 <= LDS, "ring layout");
 };
 
 TT_DEV uint4 frag_kc64(const char* img, int r0) {  // A fragment of a 32-deep, 64-byte-row image
@@ -618,7 +624,7 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
     } else {
       const int sub = (pc - 8) >> 3, kl = q >> 4;
       prow[j] = -1;
-      pcol[j] = kl * H + sub * 128 + (((q & 15) ^ (ttg::ko_v(kl) << 1)) * 8);
+      pcol[j] = kl * H + sub * 128 + (((q & 15) ^ (ttg::ko_v(kl) << 1)) * 8);  // + the pass's first unit
     }
   }
   const int jg = (tid % C::TPR) * 8, rsub = tid / C::TPR;
@@ -636,6 +642,8 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
     const int tn = R.dir ? t - 1 : t + 1;
     const int tp = R.dir ? t + 1 : t - 1;
     const bool last = (s == T_ - 1);
+    // one column pass: units [u0, u0 + HP)
+    auto column_pass = [&](const int u0) {
     f32x4 acc[4][C::NCB];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -664,7 +672,7 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
             src = hi ? as1[j] : as0[j];
             if (src != zp) src += (long)r * 64;  // 32 k of bf16
           } else {
-            src = reinterpret_cast<const char*>(W + (long)r * 32 * H + pcol[j]);
+            src = reinterpret_cast<const char*>(W + (long)r * 32 * H + u0 + pcol[j]);
           }
           ttg::dma16(src, img + (uint32_t)pc * 1024u);
         }
@@ -681,8 +689,8 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
         uint4 fa[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) fa[i] = frag_kc64(sl, wr * 64 + 16 * i);
-        const char* ib = sl + 8192 + ((wc * (H / 4)) >> 7) * 8192;
-        const int cb = (wc * (H / 4)) & 127;
+        const char* ib = sl + 8192 + ((wc * (C::HP / 4)) >> 7) * 8192;
+        const int cb = (wc * (C::HP / 4)) & 127;
 #pragma unroll
         for (int jp = 0; jp < C::NCB; jp += 2) {
           uint4 fb[2];
@@ -717,7 +725,7 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
         const uint32_t w0 = (uint32_t)f2bf(acc[i][jc][0]) | ((uint32_t)f2bf(acc[i][jc][1]) << 16);
         const uint32_t w1 = (uint32_t)f2bf(acc[i][jc][2]) | ((uint32_t)f2bf(acc[i][jc][3]) << 16);
         *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(lds) + (wr * 64 + 16 * i + (lane & 15)) * C::LDB +
-                                  wc * (H / 4) + 16 * jc + 4 * (lane >> 4)) = make_uint2(w0, w1);
+                                  wc * (C::HP / 4) + 16 * jc + 4 * (lane >> 4)) = make_uint2(w0, w1);
       }
     __syncthreads();
     float bsum[4][8];
@@ -733,9 +741,9 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
       for (int kk = 0; kk < NB; ++kk) {
         const int bl = rsub + C::RPI * (kb + kk);
         const bool ok = m0 + bl < a.B && !(dbg & 2);
-        const uint32_t oc = ok ? (uint32_t)(bl * H + jg) * 2u : 0x80000000u;
-        const uint32_t oy = ok ? (uint32_t)(bl * T_ * (int)a.ldy + jg) * 2u : 0x80000000u;
-        const uint32_t os = ok ? (uint32_t)(bl * T_ * 4 * H + jg) * 2u : 0x80000000u;
+        const uint32_t oc = ok ? (uint32_t)(bl * H + u0 + jg) * 2u : 0x80000000u;
+        const uint32_t oy = ok ? (uint32_t)(bl * T_ * (int)a.ldy + u0 + jg) * 2u : 0x80000000u;
+        const uint32_t os = ok ? (uint32_t)(bl * T_ * 4 * H + u0 + jg) * 2u : 0x80000000u;
         vin[kk][0] = ld16_buf(rc, oc, 0);
         vin[kk][1] = ld16_buf(rd, oy, 0);
 #pragma unroll
@@ -756,7 +764,7 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
         unpack8(vin[kk][5], gh);
         unpack8(vin[kk][6], hp);
         unpack8(*reinterpret_cast<const uint4*>(L16 + ((bl * C::LDB + jg) >> 1)), gm);
-        if (last && R.dfinal) ld8(R.dfinal + (long)b * a.ldf + jg, cin);
+        if (last && R.dfinal) ld8(R.dfinal + (long)b * a.ldf + u0 + jg, cin);
         float o_r[8], o_z[8], o_n[8], o_hn[8], cout[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -776,13 +784,13 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
           if (o_r[0] == 12345.f) L16[0] = __float_as_uint(o_z[1] + o_n[2] + o_hn[3] + cout[4]);
           continue;
         }
-        st8(cr_cur + (long)bl * H + jg, cout);
+        st8(cr_cur + (long)bl * H + u0 + jg, cout);
         const long row = (long)b * T_ + t;
-        bf16_t* xw = DGXw + row * a.ldd + jg;
+        bf16_t* xw = DGXw + row * a.ldd + u0 + jg;
         st8(xw, o_r);
         st8(xw + H, o_z);
-        st8_sc1(grs, (int)(((long)bl * T_ * a.ldd + jg + 2 * H) * 2L), o_n, (bf16_t*)nullptr);
-        st8(DGHw + row * a.ldd + jg, o_hn);
+        st8_sc1(grs, (int)(((long)bl * T_ * a.ldd + u0 + jg + 2 * H) * 2L), o_n, (bf16_t*)nullptr);
+        st8(DGHw + row * a.ldd + u0 + jg, o_hn);
       }
     }
     __syncthreads();
@@ -790,16 +798,23 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) red[(rsub * 4 + q) * H + jg + e] = bsum[q][e];
+      for (int e = 0; e < 8; ++e) red[(rsub * 4 + q) * C::HP + jg + e] = bsum[q][e];
     __syncthreads();
-    for (int c = tid; c < 4 * H; c += 512) {
+    for (int c = tid; c < 4 * C::HP; c += 512) {
       float v = 0.f;
 #pragma unroll
-      for (int w = 0; w < C::RPI; ++w) v += red[w * 4 * H + c];
-      part[c] += v;
+      for (int w = 0; w < C::RPI; ++w) v += red[w * 4 * C::HP + c];
+      part[(c / C::HP) * H + u0 + c % C::HP] += v;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    };
+    if constexpr (C::NP == 1) {
+      column_pass(0);
+    } else {
+#pragma unroll 1
+      for (int pass = 0; pass < C::NP; ++pass) column_pass(pass * C::HP);
+    }
   }
 }
 
@@ -1587,7 +1602,8 @@ extern "C" int tt_gru_bias_rows(int B) { return tt_ceil_div(B, bwd_rows()); }
 extern "C" int tt_gru_fwd_launches(int dtype, int T, int H) { return gru_fwd_persistent(dtype, H) ? 1 : T; }
 
 static bool gru_bwd_persistent(int dtype, int H) {
-  return dtype == TT_DT_BF16 && (H == 256 || H == 512) && bwd_rows() == 128 && tt::opt(tt::OPT_GRU_BWD_PERSIST) != 0;
+  return dtype == TT_DT_BF16 && (H == 256 || H == 512 || H == 1024) && bwd_rows() == 128 &&
+         tt::opt(tt::OPT_GRU_BWD_PERSIST) != 0;
 }
 extern "C" int tt_gru_bwd_launches(int dtype, int T, int H) { return gru_bwd_persistent(dtype, H) ? 1 : T; }
 
@@ -1861,7 +1877,8 @@ extern "C" int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B
   if (gru_bwd_persistent(dtype, H)) {
     TT_CHECK_ARG(128L * T * std::max({ldd, ldy, 4L * H}) * esz < (1L << 31), "tt_gru_bwd: tile offsets exceed 2 GiB");
     const dim3 grid(tt_ceil_div(B, 128) * nrec);
-    if (H == 512) hipLaunchKernelGGL(gru_bwd_rows<512>, grid, dim3(512), 0, st, a);
+    if (H == 1024) hipLaunchKernelGGL(gru_bwd_rows<1024>, grid, dim3(512), 0, st, a);
+    else if (H == 512) hipLaunchKernelGGL(gru_bwd_rows<512>, grid, dim3(512), 0, st, a);
     else hipLaunchKernelGGL(gru_bwd_rows<256>, grid, dim3(512), 0, st, a);
     TT_CHECK_LAUNCH("gru_bwd_rows");
     return 0;

@@ -147,8 +147,7 @@ def test_reference_size_h512_bf16_matches_oracle():
     """hidden_dim 512 (GRU H = 1024), the reference's own training size
     (train_enhanced.py:30) and BASELINE configs[4]'s model, in bf16 at T = 32 (configs[4]
     runs T = 128): the per-step bf16 forward (H > 512 exceeds the row-resident kernel's
-    LDS image) and the row-owning BPTT (gru_bwd_rows<1024>, two column passes per step),
-    against the fp32 oracle on
+    LDS image) and the 256x256 BPTT step kernel (gru_bwd_big), against the fp32 oracle on
     bf16-rounded operands, with the tolerances stated at the top of this file."""
     Hd, Tq, Bq = 512, 32, 64
     torch.manual_seed(35)
@@ -244,8 +243,7 @@ def test_reference_size_h512_t128_bf16_matches_oracle():
     """configs[4]'s model and sequence length: hidden_dim 512 (GRU H = 1024,
     train_enhanced.py:30, enhanced_two_tower.py:19), T = 128, bf16, dropout 0.1, B = 16,
     InfoNCE + backward, against the fp32 oracle on bf16-rounded operands. Runs the kernels
-    configs[4] runs (per-step bf16 forward, row-owning BPTT in two column passes) over 128
-    steps, so the
+    configs[4] runs (per-step bf16 forward, 256 x 256 per-step BPTT) over 128 steps, so the
     bf16 rounding of the recurrent state, the saved pre-activations and the BPTT carry
     compounds over twice the steps of the bench configuration; tolerances as stated at the
     top of this file."""

@@ -12,3 +12,10 @@ import json
 for f in ('r4c_bench','r4c_bench_nobres','r4c_bench_c4','r4c_bench_c4_old'):
     d=json.load(open('gpurun_out/'+f+'.json')); k=d['kernel_ms_per_step']; print(f, d['value'], d['ms_per_step'], {n:k[n]['ms_per_step'] for n in k})
 "
+for v in "" "TT_GRU_BWD_ROWS=64" "TT_GRU_BWD_STREAMS=1"; do
+  env $v timeout -k 10 300 python bench.py --batch 1024 --dtype fp32 --loss infonce --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/r4c_bench_c1.json 2>> gpurun_out/r4c_bench.err || exit 1
+  python3 -c "
+import json,sys
+d=json.load(open('gpurun_out/r4c_bench_c1.json')); k=d['kernel_ms_per_step']; print('c1 $v', d['value'], d['ms_per_step'], {n:k[n]['ms_per_step'] for n in k})
+"
+done

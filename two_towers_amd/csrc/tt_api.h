@@ -15,7 +15,7 @@ void set_error(const char* fmt, ...);
 enum Opt {
   OPT_GRU_STEP,         // 1: per-step GRU forward even where the persistent kernel applies
   OPT_GRU_DEPTH,        // persistent forward W_hh ring depth cap (1, 2, 4)
-  OPT_GRU_BWD_ROWS,     // 128 or 64 batch rows per backward step tile
+  OPT_GRU_BWD_ROWS,     // 128 or 64 batch rows per backward step tile (0: by grid size)
   OPT_GRU_BWD_BIG,      // 0: 128x128 backward step kernels instead of 256x256
   OPT_GRU_BWD_STREAMS,  // 1: one stream chain for the 128x128 backward
   OPT_GEMM_PERSIST,     // 0: no persistent short-K GEMM
@@ -23,7 +23,7 @@ enum Opt {
   OPT_GEMM_REGSTAGE,    // 1/2: force register staging / 128-tiles (9: no epilogue, timing)
   OPT_GEMM_STREAM_OUT,  // 0: no write-through output stores
   OPT_HN_GEMM,          // 1: hard-negative top-k through GEMM + split top-k, no scan
-  OPT_GRU_BWD_PERSIST,  // 0: per-step backward launches instead of the row-owning kernel
+  OPT_GRU_BWD_PERSIST,  // 0: per-step backward launches instead of the row-owning kernel; 2: also at H 1024
   OPT_GRU_FWD_STEP_ROWS, // per-step GRU forward batch rows per tile: 128, 256 (0: by size)
   OPT_INFONCE_FLASH,    // 0: InfoNCE backward through a materialised dS (bf16, h 128/256 default fused)
   OPT_HN_MAP,           // hn_scan block -> (row tile, split) map: 0 split per XCD, 1 row tile per XCD

@@ -28,7 +28,7 @@ struct OptDef {
 };
 constexpr OptDef kOpts[OPT_N] = {
     {"gru_step", "TT_GRU_STEP", 0},               {"gru_depth", "TT_GRU_DEPTH", 4},
-    {"gru_bwd_rows", "TT_GRU_BWD_ROWS", 128},     {"gru_bwd_big", "TT_GRU_BWD_BIG", 1},
+    {"gru_bwd_rows", "TT_GRU_BWD_ROWS", 0},     {"gru_bwd_big", "TT_GRU_BWD_BIG", 1},
     {"gru_bwd_streams", "TT_GRU_BWD_STREAMS", 2}, {"gemm_persist", "TT_GEMM_PERSIST", 1},
     {"gemm_a3", "TT_GEMM_A3", 1},                 {"gemm_regstage", "TT_GEMM_REGSTAGE", 0},
     {"gemm_stream_out", "TT_GEMM_STREAM_OUT", 1}, {"hn_gemm", "TT_HN_GEMM", 0},

@@ -1595,15 +1595,27 @@ bool gru_fwd_persistent(int dtype, int H) {
 
 // batch rows per backward tile: 128, or 64 with option gru_bwd_rows = 64 (3 workgroups
 // per CU; measured slower at B=8192, H=512: 13.6 vs 11.5 ms per layer)
-static int bwd_rows() { return tt::opt(tt::OPT_GRU_BWD_ROWS) == 64 ? 64 : 128; }
-// partial bias rows: one per backward row tile
-extern "C" int tt_gru_bias_rows(int B) { return tt_ceil_div(B, bwd_rows()); }
+// Per-step backward tile rows: option gru_bwd_rows 64 / 128, or 0 (auto): 64 where 128-row
+// tiles would leave the grid under one workgroup per CU (configs[1]: B 1024, fp32, H 512 ->
+// 128 workgroups; 64-row tiles: gru_bwd 26.1 -> 15.4 ms per step, profiles/r04_bench_c1_c.txt)
+static int bwd_rows(int B, int H, int nrec) {
+  const int o = tt::opt(tt::OPT_GRU_BWD_ROWS);
+  if (o == 64 || o == 128) return o;
+  return (long)tt_ceil_div(H, 128) * tt_ceil_div(B, 128) * nrec < 256 ? 64 : 128;
+}
+// partial bias rows: one per backward row tile (the smallest tile: 64 rows; rows of a
+// larger-tile launch past its tile count are zero-filled by tt_gru_bwd and add nothing)
+extern "C" int tt_gru_bias_rows(int B) { return tt_ceil_div(B, 64); }
 
 extern "C" int tt_gru_fwd_launches(int dtype, int T, int H) { return gru_fwd_persistent(dtype, H) ? 1 : T; }
 
+// bf16 H 256 / 512 (and H 1024 in two column passes with option gru_bwd_persist = 2: measured
+// slower than the per-step 256x256 kernel at configs[4], 97.0 vs 92.9 ms per step,
+// profiles/r04_bench_c4_c.txt)
 static bool gru_bwd_persistent(int dtype, int H) {
-  return dtype == TT_DT_BF16 && (H == 256 || H == 512 || H == 1024) && bwd_rows() == 128 &&
-         tt::opt(tt::OPT_GRU_BWD_PERSIST) != 0;
+  const int o = tt::opt(tt::OPT_GRU_BWD_PERSIST);
+  return dtype == TT_DT_BF16 && (H == 256 || H == 512 || (H == 1024 && o == 2)) &&
+         tt::opt(tt::OPT_GRU_BWD_ROWS) != 64 && o != 0;
 }
 extern "C" int tt_gru_bwd_launches(int dtype, int T, int H) { return gru_bwd_persistent(dtype, H) ? 1 : T; }
 
@@ -1871,7 +1883,7 @@ extern "C" int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B
 #ifdef TT_DIAG
   if (const char* e = getenv("TT_GRU_DBG")) a.dbg = atoi(e);
 #endif
-  const int bmr = bwd_rows();
+  const int bmr = bwd_rows(B, H, nrec);
   // bf16, H 256 / 512: one row-owning launch per layer (option gru_bwd_persist = 0: per-step
   // launches)
   if (gru_bwd_persistent(dtype, H)) {

@@ -123,11 +123,15 @@ def cpu_baseline(args):
         loss.backward()
         opt.step()
 
-    for _ in range(args.cpu_warmup):
+    import sys
+    for i in range(args.cpu_warmup):
         step()
+        print(f"cpu baseline: warm-up step {i + 1}/{args.cpu_warmup} done", file=sys.stderr, flush=True)
     t0 = time.perf_counter()
-    for _ in range(args.cpu_steps):
+    for i in range(args.cpu_steps):
         step()
+        print(f"cpu baseline: step {i + 1}/{args.cpu_steps} done ({time.perf_counter() - t0:.1f} s)", file=sys.stderr,
+              flush=True)
     dt = time.perf_counter() - t0
     cpu = platform.processor() or platform.machine()
     try:

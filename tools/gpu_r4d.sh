@@ -1,0 +1,13 @@
+mkdir -p gpurun_out
+timeout -k 10 1200 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > gpurun_out/r4d_pytest.txt 2>&1; rc=$?; tail -3 gpurun_out/r4d_pytest.txt
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4d_smoke.txt 2>&1 || exit 1
+timeout -k 10 300 python tools/bench_gru.py --variants "" --bwd-variants P:0:2:0,P:0:2:14,P:0:2:-7,P:0:2:-5,P:0:2:-9,P:0:2:14,P:0:2:-7 --iters 5 > gpurun_out/r4d_skew.txt 2>&1 || exit 1
+cat gpurun_out/r4d_skew.txt
+for v in "" "TT_GRU_BWD_STREAMS=1" "TT_GRU_FWD_STEP_ROWS=256" "TT_GRU_FWD_STEP_ROWS=128"; do
+  env $v timeout -k 10 300 python bench.py --batch 1024 --dtype fp32 --loss infonce --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/r4d_bench_c1.json 2>> gpurun_out/r4d_bench.err || exit 1
+  python3 -c "
+import json,sys
+d=json.load(open('gpurun_out/r4d_bench_c1.json')); k=d['kernel_ms_per_step']; print('c1 $v', d['value'], d['ms_per_step'], {n:k[n]['ms_per_step'] for n in k})
+"
+done

@@ -607,8 +607,12 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
   constexpr int NK = 3 * H / 32;  // 32-deep K-tiles per step
   // workgroups in lockstep put every CU in its product phase (L2-bound) at the same time and
   // then in its HBM-bound epilogue; a start skew for half of them interleaves the phases
-  if (a.skew > 0 && ((blockIdx.x >> 3) & 1))
-    for (int i = 0; i < a.skew; ++i) __builtin_amdgcn_s_sleep(127);
+  // (skew < 0: four phases, |skew| apart)
+  if (a.skew != 0) {
+    const int ph = a.skew > 0 ? (int)((blockIdx.x >> 3) & 1) : (int)((blockIdx.x >> 3) & 3);
+    const int n = ph * (a.skew > 0 ? a.skew : -a.skew);
+    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   const long ldr = (long)T_ * a.ldd;
   // DMA pieces of a slot, wave + 8j (j < P): piece 0..7 = the A image (row q >> 2, chunk
   // slot q & 3 of 16-byte unit q), then NQ x 8 pieces of W_hh sub-images (k-row q >> 4,

@@ -277,3 +277,62 @@ def test_two_rank_dropout_masks_are_global_batch_masks():
     with torch.no_grad():
         qe, _ = m.eval()(torch.from_numpy(z["q"]).cuda(), torch.from_numpy(z["d"]).cuda())
     assert float((qe.cpu() - torch.from_numpy(q1)).abs().max()) > 1e-4
+
+
+def _bench_scale_rank(port, use_pg, out):
+    """One bench-composition step at bench scale (E 300, h 256, T 64, bf16, dropout 0.1,
+    B 1024, hard-negative margin loss, Adam) with the column-split GRU forward, either
+    plain or inside a one-rank RCCL process group with every collective forced on."""
+    import numpy as np
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    if use_pg:
+        os.environ["TT_DIST_FORCE"] = "1"
+        torch.distributed.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        import two_towers_amd as tta
+        from two_towers_amd import _lib
+        from two_towers_amd import dist as tdp
+        _lib.set_option("gru_fwd_xc", 1)
+        torch.manual_seed(5)
+        m = tta.EnhancedTwoTowerModel(300, 256).cuda().set_compute_dtype(torch.bfloat16).train()
+        m.set_process_group(None, overlap_grad_allreduce=True)
+        assert _lib.load().tt_gru_fwd_ws_size(_lib.DT_BF16, 4, 1024, 64, 512, 3072, 1024) > 0, "xcp expected"
+        g = torch.Generator().manual_seed(6)
+        q = (torch.randn(1024, 64, 300, generator=g) * 0.5).cuda()
+        d = (torch.randn(1024, 64, 300, generator=g) * 0.5).cuda()
+        crit = tta.HardNegativeMarginLoss(k=5, margin=0.2, compute_dtype=torch.bfloat16)
+        opt = tta.Adam(m.parameters(), lr=1e-3)
+        torch.manual_seed(7)
+        loss = crit(*m(q, d))
+        loss.backward()
+        tdp.allreduce_grads(list(m.parameters()))
+        opt.step()
+        tta.check_gru_status()
+        out.put((float(loss.detach()), {k: v.detach().cpu().float().numpy().copy() for k, v in m.state_dict().items()},
+                 crit.last_indices.cpu().numpy().copy()))
+    finally:
+        if use_pg:
+            torch.distributed.destroy_process_group()
+
+
+def test_rccl_one_rank_bench_scale_step_is_bit_identical():
+    """The bench's kernels under a process group: the column-split forward, the streamed
+    hard-negative scan, the overlapped gradient all-reduce on RCCL's stream. With one rank
+    every collective is an identity, so the loss, the mined indices and every weight after
+    Adam must be bit-identical to the same step without a process group."""
+    import numpy as np
+    ctx = mp.get_context("spawn")
+    res = []
+    for use_pg in (False, True):
+        out = ctx.Queue()
+        p = ctx.Process(target=_bench_scale_rank, args=(_port(), use_pg, out))
+        p.start()
+        res.append(out.get(timeout=240))
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (l0, w0, i0), (l1, w1, i1) = res
+    assert l0 == l1, (l0, l1)
+    assert (i0 == i1).all()
+    for k in w0:
+        assert np.array_equal(w0[k], w1[k]), k

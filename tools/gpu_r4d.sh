@@ -11,3 +11,6 @@ import json,sys
 d=json.load(open('gpurun_out/r4d_bench_c1.json')); k=d['kernel_ms_per_step']; print('c1 $v', d['value'], d['ms_per_step'], {n:k[n]['ms_per_step'] for n in k})
 "
 done
+# gru_bwd_rows phase diagnostics (diag build: 1 no GEMM, 2 no epilogue loads, 4 no stores), skew 14 default
+TT_HIP_LIB=two_towers_amd/lib/libtt_hip_diag.so timeout -k 10 300 python tools/bench_gru.py --variants "" --bwd-variants P:0:2:14,P:1:2:14,P:2:2:14,P:4:2:14,P:6:2:14,P:7:2:14,P:0:2:0,P:1:2:0,P:6:2:0 --iters 5 > gpurun_out/r4d_bwd_diag.txt 2>&1 || exit 1
+cat gpurun_out/r4d_bwd_diag.txt

@@ -121,6 +121,22 @@ def test_hardneg_scan_matches_gemm_path(B, nd, h, lab):
     assert torch.equal(si, gi)
 
 
+@pytest.mark.parametrize("B,nd,lab", [(8192, 8192, 0), (2048, 16384, 100), (1000, 3000, 0)])
+@pytest.mark.parametrize("hn_map", [1, 2])
+def test_hardneg_scan_block_maps_agree(B, nd, lab, hn_map):
+    """The scan's workgroup -> (row tile, document split) maps (option hn_map: 0 a split
+    per XCD, 1 a row tile per XCD, 2 row-tile halves x split quarters per XCD; 2 falls back
+    to 0 where the grid does not divide) only move work between workgroups: bit-identical."""
+    g = torch.Generator().manual_seed(B + nd + hn_map)
+    q = torch.nn.functional.normalize(torch.randn(B, 256, generator=g), dim=1)
+    d = torch.nn.functional.normalize(torch.randn(nd, 256, generator=g), dim=1)
+    si, sv = run_hardneg(q, d, lab, 5, torch.bfloat16)
+    with option("hn_map", hn_map):
+        mi, mv = run_hardneg(q, d, lab, 5, torch.bfloat16)
+    assert torch.equal(sv, mv)
+    assert torch.equal(si, mi)
+
+
 def test_hardneg_hot_chunks():
     """Correlated rows (every query closest to the same few documents, as with a freshly
     initialised tower): all rows select the same chunks, so the rescoring of one chunk

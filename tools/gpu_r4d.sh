@@ -14,3 +14,8 @@ done
 # gru_bwd_rows phase diagnostics (diag build: 1 no GEMM, 2 no epilogue loads, 4 no stores), skew 14 default
 TT_HIP_LIB=two_towers_amd/lib/libtt_hip_diag.so timeout -k 10 300 python tools/bench_gru.py --variants "" --bwd-variants P:0:2:14,P:1:2:14,P:2:2:14,P:4:2:14,P:6:2:14,P:7:2:14,P:0:2:0,P:1:2:0,P:6:2:0 --iters 5 > gpurun_out/r4d_bwd_diag.txt 2>&1 || exit 1
 cat gpurun_out/r4d_bwd_diag.txt
+# hn_scan block maps: 0 split per XCD (default), 1 row tile per XCD, 2 row halves x split quarters per XCD
+for rep in 1 2; do
+timeout -k 10 200 python tools/bench_score.py --ops hardneg --iters 50 --hn-shapes 8192x8192x256,8192x65536x256 --variants "map1=hn_map=1;map2=hn_map=2" >> gpurun_out/r4d_hnmap.txt 2>&1 || exit 1
+done
+cat gpurun_out/r4d_hnmap.txt

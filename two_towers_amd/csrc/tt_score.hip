@@ -150,8 +150,20 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
   // map 0: blocks round-robin over the XCDs, so split b % S stays on one XCD and its
   // document slice in that L2; map 1 (option hn_map): the S splits of a row tile share an
   // XCD (xcd_remap), so the tile's query rows are fetched into that L2 once
-  const int bid = map ? ttg::xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-  const int split = bid % S, rt = bid / S;
+  // map 2: XCD x (= b % 8) owns row-tile half x & 1 and split quarter x >> 1, so each XCD
+  // reads half of Q and a quarter of D (8 x 3 MB from HBM at 8192^2 x 256 instead of 8 x
+  // 4.5 MB: the query prologue, every CU at once, is HBM-bound); needs RT % 2 == 0 and
+  // S % 4 == 0 (the host falls back to map 0 otherwise)
+  int split, rt;
+  if (map == 2) {
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3, sq = S >> 2;
+    split = (x >> 1) * sq + j % sq;
+    rt = (x & 1) * (int)(gridDim.x / S / 2) + j / sq;
+  } else {
+    const int bid = map ? ttg::xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    split = bid % S;
+    rt = bid / S;
+  }
   const long t0 = (long)split * tps;
   const int nt = (int)(nch - t0 < tps ? nch - t0 : tps);
   if (nt <= 0) return;
@@ -521,8 +533,10 @@ int hn_run(const bf16_t* qn, long bq, const bf16_t* dn, long nd, long label_offs
   int32_t* sel = reinterpret_cast<int32_t*>(ws + p.off_sel);
   float* cand = reinterpret_cast<float*>(ws + p.off_cand);
   const int nsel = (int)(p.nch < k ? p.nch : k);
+  int map = tt::opt(tt::OPT_HN_MAP);
+  if (map == 2 && (p.RT % 2 != 0 || p.S % 4 != 0)) map = 0;
   hipLaunchKernelGGL((hn_scan_kernel<KS>), dim3((unsigned)(p.RT * p.S)), dim3(ScanCfg<KS>::WAVES * 64), 0, st, qn, bq, dn, nd, label_offset, (int)p.S,
-                     (int)p.tps, p.nch, CM, tt::opt(tt::OPT_HN_MAP));
+                     (int)p.tps, p.nch, CM, map);
   TT_CHECK_LAUNCH("hn_scan_kernel");
   const dim3 rows4((unsigned)tt_ceil_div(bq, 4));
   if (k <= 8)

@@ -1,5 +1,5 @@
 mkdir -p gpurun_out
-timeout -k 10 1200 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > gpurun_out/r4d_pytest.txt 2>&1; rc=$?; tail -3 gpurun_out/r4d_pytest.txt
+timeout -k 10 1200 python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests > gpurun_out/r4d_pytest.txt 2>&1; rc=$?; tail -3 gpurun_out/r4d_pytest.txt
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4d_smoke.txt 2>&1 || exit 1
 timeout -k 10 300 python tools/bench_gru.py --variants "" --bwd-variants P:0:2:0,P:0:2:14,P:0:2:-7,P:0:2:-5,P:0:2:-9,P:0:2:14,P:0:2:-7 --iters 5 > gpurun_out/r4d_skew.txt 2>&1 || exit 1
@@ -19,3 +19,6 @@ for rep in 1 2; do
 timeout -k 10 200 python tools/bench_score.py --ops hardneg --iters 50 --hn-shapes 8192x8192x256,8192x65536x256 --variants "map1=hn_map=1;map2=hn_map=2" >> gpurun_out/r4d_hnmap.txt 2>&1 || exit 1
 done
 cat gpurun_out/r4d_hnmap.txt
+# hn_scan query prologue overlapped with tile 0 (libtt_hip, HN_PIPE_Q=1) vs retired up front (libtt_hip_exp, HN_PIPE_Q=0)
+bash tools/ab_scan.sh r4d libtt_hip.so libtt_hip_exp.so > gpurun_out/r4d_scan.txt 2>&1 || exit 1
+cat gpurun_out/r4d_scan.txt

@@ -41,6 +41,9 @@ constexpr int SC_COLS = 64;     // document columns per tile (= per chunk)
 #ifndef HN_W4
 #define HN_W4 1
 #endif
+#ifndef HN_PIPE_Q  // query prologue overlapped with the first tile (0: retired up front, round-4 form)
+#define HN_PIPE_Q 1
+#endif
 constexpr int SC_TPS_MAX = 32;  // tiles per workgroup (chunk-max staging)
 
 // Per width (h = 32 KS). h <= 256: 8 waves (two per SIMD, 256 query rows per workgroup)
@@ -170,25 +173,42 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const long row0 = (long)rt * SC_ROWS + wave * (SC_RB * 16);
   constexpr int h = 32 * KS;
-  // The first two tiles are requested before the query rows, so their latency overlaps.
+  // The first tiles are requested before the query rows, so their latency overlaps. With
+  // the 4-slot ring (PQ: the default h 256 form) all four slots are filled up front and the
+  // query fragments are loaded k-step by k-step after them and NOT retired here: tile 0's
+  // k-step ks waits (hipcc's own counted vmcnt) only for the fragments of k-steps <= ks,
+  // so the query prologue overlaps the first tile's MFMAs. The waits are exact: every DMA
+  // in flight then is older than the query loads, and none is issued before tile 2's
+  // barrier, by which time tile 0 has consumed every fragment.
   ScanDma<KS> dm;
   dm.init();
   const uint32_t lbase = __builtin_amdgcn_readfirstlane(ttg::lds_addr_of(lds));
-  dm.issue(D, nd, t0 * SC_COLS, lbase);
-  if (SC_SLOTS == 4 && nt > 1) dm.issue(D, nd, (t0 + 1) * SC_COLS, lbase + TI::BYTES);
+  constexpr bool PQ = SC_SLOTS == 4 && HN_PIPE_Q;
+  const int npre = PQ ? (nt < 4 ? nt : 4) : (SC_SLOTS == 4 && nt > 1 ? 2 : 1);
+  for (int i = 0; i < npre; ++i) dm.issue(D, nd, (t0 + i) * SC_COLS, lbase + (uint32_t)i * TI::BYTES);
+  // query fragments by buffer loads: a row past bq reads zero through the resource's range
+  // check instead of a branch, so every wave issues exactly SC_RB * KS loads (the counted
+  // wait in sync(0) relies on it)
+  const __amdgpu_buffer_rsrc_t qrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(Q), (short)0, (int)(bq * h * 2), 0x00020000);
   uint4 qa[SC_RB][KS];
 #pragma unroll
-  for (int qb = 0; qb < SC_RB; ++qb)
+  for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-      qa[qb][ks] = (HN_DIAG & 8) ? make_uint4(lane, ks, qb, 1) : ld_frag(Q, row0 + qb * 16 + (lane & 15), bq, h, ks);
-  // Retire the query loads here, so that hipcc does not place a vmcnt(0) inside the tile
-  // loop (it cannot see the LDS-DMAs and would wait for the tiles in flight every tile).
+    for (int qb = 0; qb < SC_RB; ++qb) {
+      const long row = row0 + qb * 16 + (lane & 15);
+      const uint32_t off = row < bq ? (uint32_t)((row * h + ks * 32 + 8 * (lane >> 4)) * 2) : 0x80000000u;
+      qa[qb][ks] = (HN_DIAG & 8) ? make_uint4(lane, ks, qb, 1) : ld16_buf(qrs, off, 0);
+    }
+  if constexpr (!PQ) {
+    // Retire the query loads here, so that hipcc does not place a vmcnt(0) inside the tile
+    // loop (it cannot see the LDS-DMAs and would wait for the tiles in flight every tile).
 #pragma unroll
-  for (int qb = 0; qb < SC_RB; ++qb)
+    for (int qb = 0; qb < SC_RB; ++qb)
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-      asm volatile("" ::"v"(qa[qb][ks].x), "v"(qa[qb][ks].y), "v"(qa[qb][ks].z), "v"(qa[qb][ks].w));
+      for (int ks = 0; ks < KS; ++ks)
+        asm volatile("" ::"v"(qa[qb][ks].x), "v"(qa[qb][ks].y), "v"(qa[qb][ks].z), "v"(qa[qb][ks].w));
+  }
 
   // Tiles travel in pairs: at every even tile, one wait + barrier retires the pair (t, t+1)
   // for every wave and frees slots (t+2)%4, (t+3)%4 (last read before this barrier), into
@@ -205,6 +225,16 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       if (t + 1 < nt) dm.issue(D, nd, (t0 + t + 1) * SC_COLS, lbase + (uint32_t)((t + 1) % 2) * TI::BYTES);
+    } else if (PQ && t == 0) {
+      // tiles 0 and 1 landed; tiles 2, 3 (issued before the query loads) and the query
+      // loads may still be in flight; tiles 2 and 3 are already requested
+      if constexpr (PQ) {
+        constexpr int QL = (HN_DIAG & 8) ? 0 : SC_RB * KS;
+        static_assert(QL + 2 * TI::DPW <= 63, "vmcnt range");
+        if (npre == 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QL + 2 * TI::DPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
     } else if ((t & 1) == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();

@@ -1,0 +1,84 @@
+"""The 256x256 GEMM's operand DMAs through buffer resources (option gemm_buf, Loop8 BUF)
+against the per-lane-pointer DMAs (gemm_buf 0): the LDS images of every consumed K-tile
+are the same bytes, so C must be bit-identical, on each path that runs the 8-phase loop --
+the persistent short-K kernel (input projections), the long-K kernel (dX), split-K TN
+with the split-column A and the time-shifted B (dW_hh) -- with ragged M and N; and equal
+to a fp32 product of the bf16-rounded operands."""
+import pytest
+import torch
+
+from two_towers_amd import ops
+from two_towers_amd._lib import option
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _both(fn):
+    outs = []
+    for buf in (0, 1):
+        with option("gemm_buf", buf):
+            outs.append(fn())
+    torch.cuda.synchronize()
+    return outs
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).abs().max() / (b.double().abs().max() + 1e-12))
+
+
+@pytest.mark.parametrize("akout,bkout", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("path", ["persist", "long_k"])
+def test_buffer_dma_gemm_is_bit_identical(akout, bkout, path):
+    # persist: >= 512 tiles of 256^2 at 16 K-tiles; long_k: 32 K-tiles (past the persistent cap)
+    m, n, k = (8200, 4136, 1024) if path == "persist" else (4200, 4136, 2048)
+    g = torch.Generator().manual_seed(31 + 2 * akout + bkout)
+    A = torch.randn(m, k, generator=g).to(torch.bfloat16)
+    B = torch.randn(n, k, generator=g).to(torch.bfloat16)
+    bias = torch.randn(n, generator=g).to(DEV)
+    Ad = (A.t().contiguous() if akout else A).to(DEV)
+    Bd = (B.t().contiguous() if bkout else B).to(DEV)
+
+    def run():
+        C = torch.empty(m, n, device=DEV, dtype=torch.bfloat16)
+        ops.gemm([Ad], [Bd], [C], m=m, n=n, k=k, lda=m if akout else k, ldb=n if bkout else k, ldc=n,
+                 a_kouter=bool(akout), b_kouter=bool(bkout), dtype=torch.bfloat16, out_dtype=torch.bfloat16,
+                 bias=[bias], splits=1)
+        return C
+
+    c0, c1 = _both(run)
+    assert torch.equal(c0, c1)
+    ref = A.to(DEV).float() @ B.to(DEV).float().t() + bias
+    assert _rel(c1.float(), ref) < 1e-2
+
+
+def test_buffer_dma_split_k_wgrad_hh_composition():
+    """dW_hh's GEMM: A = dL/dgh^T through the split-column loader (r|z columns of dG, the
+    W_hn block at column 6H), B = h_{t-1} (time-shifted, pointer DMAs), split-K."""
+    H, Bsz, T = 256, 512, 32
+    K = Bsz * T
+    g = torch.Generator().manual_seed(41)
+    dG = torch.randn(K, 8 * H, generator=g).to(torch.bfloat16).to(DEV)
+    Y = torch.randn(K, 2 * H, generator=g).to(torch.bfloat16).to(DEV)
+    a = [dG[:, d * 3 * H:] for d in range(2)]
+    a_hi = [dG[:, 6 * H + d * H:] for d in range(2)]
+    b = [Y[:, d * H:] for d in range(2)]
+
+    def run():
+        C = [torch.empty(3 * H, H, device=DEV) for _ in range(2)]
+        ops.gemm(a, b, C, m=3 * H, n=H, k=K, lda=8 * H, ldb=2 * H, ldc=H, a_kouter=True, b_kouter=True,
+                 dtype=torch.bfloat16, out_dtype=torch.float32, bshift=[-1, 1], seq_t=T, a_hi=a_hi, a_split=2 * H)
+        return C
+
+    c0, c1 = _both(run)
+    for d in range(2):
+        assert torch.equal(c0[d], c1[d]), d
+        dgh = torch.cat([a[d][:, :2 * H], a_hi[d][:, :H]], 1).float()
+        h = b[d].float().view(Bsz, T, H)
+        hs = torch.zeros_like(h)
+        if d == 0:
+            hs[:, 1:] = h[:, :-1]
+        else:
+            hs[:, :-1] = h[:, 1:]
+        ref = dgh.t() @ hs.reshape(K, H)
+        assert _rel(c1[d], ref) < 1e-5, (d, _rel(c1[d], ref))

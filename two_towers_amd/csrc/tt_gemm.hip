@@ -38,6 +38,7 @@ constexpr OptDef kOpts[OPT_N] = {
     {"gru_fwd_xc", "TT_GRU_FWD_XC", 1},           {"gru_xc_skip", "TT_GRU_XC_SKIP", 0},
     {"gru_xc_spins", "TT_GRU_XC_SPINS", 22},      {"gru_bwd_skew", "TT_GRU_BWD_SKEW", 14},
     {"gru_fwd_skew", "TT_GRU_FWD_SKEW", 0},       {"gemm_bres", "TT_GEMM_BRES", 1},
+    {"gemm_buf", "TT_GEMM_BUF", 1},
 };
 struct OptTable {
   std::atomic<int> v[OPT_N];
@@ -112,11 +113,12 @@ using ttg::xcd_remap;
 #endif
 
 template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO, int TBM, int TBN, int WGM, int WGN, bool DMA,
-          bool A3 = false>
+          bool A3 = false, bool BUF = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_kernel(GemmArgs g) {
   using ML = std::conditional_t<
       DMA,
-      std::conditional_t<TBM == 256 && TBN == 256 && WGM == 2 && WGN == 4, ttg::Loop8<T, AKO, BKO, TT_GEMM_BAL, A3>,
+      std::conditional_t<TBM == 256 && TBN == 256 && WGM == 2 && WGN == 4,
+                         ttg::Loop8<T, AKO, BKO, TT_GEMM_BAL, A3, false, BUF>,
                          ttg::DLoop<T, AKO, BKO, TBM, TBN, WGM, WGN>>,
       ttg::MainLoop<T, AKO, BKO, TBM, TBN>>;
   static_assert(DMA || (TBM == 128 && TBN == 128 && WGM == 2 && WGN == 2), "register path is 128x128");
@@ -512,9 +514,9 @@ __global__ __launch_bounds__(512, 1) void gemm_bres(GemmArgs g, int npan, int nb
 // first counted wait of the next tile lets the epilogue's stores stay in flight. Measured
 // before this: the LDS-staged epilogue plus its barriers cost ~20k cycles per tile, more
 // than the 5 K-tiles of MFMAs of input_proj_l0.
-template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO, bool A3>
+template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO, bool A3, bool BUF = false>
 __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
-  using L8 = ttg::Loop8<T, AKO, BKO, false, A3, A3>;  // A3: transposed accumulate, direct epilogue
+  using L8 = ttg::Loop8<T, AKO, BKO, false, A3, A3, BUF>;  // A3: transposed accumulate, direct epilogue
   using Piece = typename L8::Piece;
   constexpr int STG = A3 ? 0 : 32 * 256 * 4;
   static_assert(!A3 || 2 * L8::HALF >= 32 * 256 * 4, "staging fits an A slot");
@@ -587,31 +589,29 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
 #endif
   auto la = loader_a(w);
   auto lb = loader_b(w);
-  Piece pa0[2], pa1[2], pb0[2], pb1[2];
-  L8::template init_half<AKO>(la, 0, nk, g.K, 0, pa0);
-  L8::template init_half<AKO>(la, 0, nk, g.K, 128, pa1);
-  L8::template init_half<BKO>(lb, 0, nk, g.K, 0, pb0);
-  L8::template init_half<BKO>(lb, 0, nk, g.K, 128, pb1);
-  long da = ttg::KTB, db = ttg::KTB;
-  if constexpr (AKO) da = (long)L8::KTE * g.lda * (long)sizeof(T);
-  if constexpr (BKO) db = (long)L8::KTE * g.ldb * (long)sizeof(T);
+  typename L8::template Half<AKO, decltype(la)> pa0, pa1;
+  typename L8::template Half<BKO, decltype(lb)> pb0, pb1;
+  pa0.init(la, 0, nk, g.K, 0);
+  pa1.init(la, 0, nk, g.K, 128);
+  pb0.init(lb, 0, nk, g.K, 0);
+  pb1.init(lb, 0, nk, g.K, 128);
   if constexpr (A3) {
-    L8::issue_half(la, pa0, 0, da, base);
-    L8::issue_half(la, pa1, 0, da, base + L8::HALF);
-    L8::issue_half(lb, pb0, 0, db, base + L8::BOFF);
-    L8::issue_half(lb, pb1, 0, db, base + L8::BOFF + L8::HALF);
-    L8::issue_half(la, pa0, 1, da, base + 2 * L8::HALF);
-    L8::issue_half(la, pa1, 1, da, base + 3 * L8::HALF);
-    L8::issue_half(lb, pb0, 1, db, base + L8::BOFF + 2 * L8::HALF);
-    L8::issue_half(lb, pb1, 1, db, base + L8::BOFF + 3 * L8::HALF);
+    pa0.issue(0, base);
+    pa1.issue(0, base + L8::HALF);
+    pb0.issue(0, base + L8::BOFF);
+    pb1.issue(0, base + L8::BOFF + L8::HALF);
+    pa0.issue(1, base + 2 * L8::HALF);
+    pa1.issue(1, base + 3 * L8::HALF);
+    pb0.issue(1, base + L8::BOFF + 2 * L8::HALF);
+    pb1.issue(1, base + L8::BOFF + 3 * L8::HALF);
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   } else {
-    L8::issue_half(la, pa0, 0, da, base);
-    L8::issue_half(la, pa1, 0, da, base + L8::HALF);
-    L8::issue_half(lb, pb0, 0, db, base + 2 * L8::HALF);
-    L8::issue_half(lb, pb1, 0, db, base + 3 * L8::HALF);
-    L8::issue_half(lb, pb0, 1, db, base + L8::SLOT + 2 * L8::HALF);
-    L8::issue_half(lb, pb1, 1, db, base + L8::SLOT + 3 * L8::HALF);
+    pa0.issue(0, base);
+    pa1.issue(0, base + L8::HALF);
+    pb0.issue(0, base + 2 * L8::HALF);
+    pb1.issue(0, base + 3 * L8::HALF);
+    pb0.issue(1, base + L8::SLOT + 2 * L8::HALF);
+    pb1.issue(1, base + L8::SLOT + 3 * L8::HALF);
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
@@ -642,8 +642,8 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
         // the stream's A and B K-tile r+2 belong to tile qn once r + 2 == nk
         if (r + 2 == nk) {
           la = loader_a(qn);
-          L8::template init_half<AKO>(la, 0, nk, g.K, 0, pa0);
-          L8::template init_half<AKO>(la, 0, nk, g.K, 128, pa1);
+          pa0.init(la, 0, nk, g.K, 0);
+          pa1.init(la, 0, nk, g.K, 128);
           ra_off = nk;
         }
 #pragma unroll
@@ -653,23 +653,23 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) fb[ks][j] = ttg::frag2<T, BKO>(ib, bc + 16 * j, ks);
         }
-        L8::issue_half(la, pa0, r + 2 - ra_off, da, anx);
+        pa0.issue(r + 2 - ra_off, anx);
         L8::quad(0, 0, fa, fb, acc);
-        L8::issue_half(la, pa1, r + 2 - ra_off, da, anx + L8::HALF);
+        pa1.issue(r + 2 - ra_off, anx + L8::HALF);
         L8::quad(0, 1, fa, fb, acc);
         if (r + 2 == nk) {
           lb = loader_b(qn);
-          L8::template init_half<BKO>(lb, 0, nk, g.K, 0, pb0);
-          L8::template init_half<BKO>(lb, 0, nk, g.K, 128, pb1);
+          pb0.init(lb, 0, nk, g.K, 0);
+          pb1.init(lb, 0, nk, g.K, 128);
           rb_off = nk;
         }
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
           for (int i = 0; i < 4; ++i) fa[ks][i] = ttg::frag2<T, AKO>(ia, 64 + 16 * i, ks);
-        L8::issue_half(lb, pb0, r + 2 - rb_off, db, bcur);
+        pb0.issue(r + 2 - rb_off, bcur);
         L8::quad(1, 1, fa, fb, acc);
-        L8::issue_half(lb, pb1, r + 2 - rb_off, db, bcur + L8::HALF);
+        pb1.issue(r + 2 - rb_off, bcur + L8::HALF);
         // K-tile r+1 landed; the 8 DMAs of r+2 stay in flight, and at r = 0 also the
         // previous tile's epilogue stores (issued after r+1's DMAs, before r+2's)
 #ifdef TT_DIAG
@@ -703,8 +703,8 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
       // the stream's next A K-tile belongs to tile qn once r + 1 == nk
       if (r + 1 == nk) {
         la = loader_a(qn);
-        L8::template init_half<AKO>(la, 0, nk, g.K, 0, pa0);
-        L8::template init_half<AKO>(la, 0, nk, g.K, 128, pa1);
+        pa0.init(la, 0, nk, g.K, 0);
+        pa1.init(la, 0, nk, g.K, 128);
         ra_off = nk;
       }
       // P1
@@ -715,26 +715,26 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) fb[ks][j] = ttg::frag2<T, BKO>(ib, bc + 16 * j, ks);
       }
-      L8::issue_half(la, pa0, r + 1 - ra_off, da, nxt);
+      pa0.issue(r + 1 - ra_off, nxt);
       L8::quad(0, 0, fa, fb, acc);
       // P2
-      L8::issue_half(la, pa1, r + 1 - ra_off, da, nxt + L8::HALF);
+      pa1.issue(r + 1 - ra_off, nxt + L8::HALF);
       L8::quad(0, 1, fa, fb, acc);
       // P3: the stream's B K-tile r+2 belongs to tile qn once r + 2 == nk
       if (r + 2 == nk) {
         lb = loader_b(qn);
-        L8::template init_half<BKO>(lb, 0, nk, g.K, 0, pb0);
-        L8::template init_half<BKO>(lb, 0, nk, g.K, 128, pb1);
+        pb0.init(lb, 0, nk, g.K, 0);
+        pb1.init(lb, 0, nk, g.K, 128);
         rb_off = nk;
       }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int i = 0; i < 4; ++i) fa[ks][i] = ttg::frag2<T, AKO>(ia, 64 + 16 * i, ks);
-      L8::issue_half(lb, pb0, r + 2 - rb_off, db, cur + 2 * L8::HALF);
+      pb0.issue(r + 2 - rb_off, cur + 2 * L8::HALF);
       L8::quad(1, 1, fa, fb, acc);
       // P4
-      L8::issue_half(lb, pb1, r + 2 - rb_off, db, cur + 3 * L8::HALF);
+      pb1.issue(r + 2 - rb_off, cur + 3 * L8::HALF);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       L8::quad(1, 0, fa, fb, acc);
     }
@@ -828,11 +828,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* ws, lon
   }
 }
 
-template <typename T, typename TO, int TBM, int TBN, int WGM, int WGN, bool DMA, bool A3 = false>
+template <typename T, typename TO, int TBM, int TBN, int WGM, int WGN, bool DMA, bool A3 = false, bool BUF = false>
 int launch_t(int akout, int bkout, bool shift, const GemmArgs& g, long nwg, hipStream_t st) {
   dim3 grid((unsigned)nwg), blk(64 * WGM * WGN);
 #define TT_L(AK, BK, SH) \
-  hipLaunchKernelGGL((gemm_kernel<T, AK, BK, SH, TO, TBM, TBN, WGM, WGN, DMA, A3>), grid, blk, 0, st, g)
+  hipLaunchKernelGGL((gemm_kernel<T, AK, BK, SH, TO, TBM, TBN, WGM, WGN, DMA, A3, BUF>), grid, blk, 0, st, g)
   if (!akout && !bkout) TT_L(false, false, false);
   else if (!akout && bkout && !shift) TT_L(false, true, false);
   else if (!akout && bkout && shift) TT_L(false, true, true);
@@ -849,13 +849,15 @@ int launch_t(int akout, int bkout, bool shift, const GemmArgs& g, long nwg, hipS
 inline bool use_big(int m, int n, long tiles256) { return m >= 256 && n >= 256 && tiles256 >= 256; }
 
 template <typename T, typename TO>
-int launch_persist(int akout, int bkout, bool shift, const GemmArgs& g, int ntiles, hipStream_t st) {
+int launch_persist(int akout, int bkout, bool shift, const GemmArgs& g, int ntiles, bool buf, hipStream_t st) {
   dim3 grid((unsigned)std::min(ntiles, 256)), blk(512);
-#define TT_L(AK, BK, SH, A3) hipLaunchKernelGGL((gemm_persist<T, AK, BK, SH, TO, A3>), grid, blk, 0, st, g, ntiles)
+#define TT_L(AK, BK, SH, A3, BUF) \
+  hipLaunchKernelGGL((gemm_persist<T, AK, BK, SH, TO, A3, BUF>), grid, blk, 0, st, g, ntiles)
 #define TT_L2(AK, BK, SH) \
   do {                     \
-    if (a3) TT_L(AK, BK, SH, true); \
-    else TT_L(AK, BK, SH, false);   \
+    if (a3 && buf) TT_L(AK, BK, SH, true, sizeof(T) == 2); \
+    else if (a3) TT_L(AK, BK, SH, true, false); \
+    else TT_L(AK, BK, SH, false, false);   \
   } while (0)
   const bool a3 = tt::opt(tt::OPT_GEMM_A3) != 0;
   if (!akout && !bkout) TT_L2(false, false, false);
@@ -917,10 +919,30 @@ int launch_gemm(int akout, int bkout, bool shift, GemmArgs& g, int nbatch, hipSt
   // slower at 48 and 128), no split-K, no accumulate (env TT_GEMM_PERSIST=0 disables)
   const bool persist_ok = tt::opt(tt::OPT_GEMM_PERSIST) != 0;
   const int nk = (g.K * (int)sizeof(T) + ttg::KTB - 1) / ttg::KTB;
+  // operand DMAs through buffer resources (Loop8 BUF): bf16, whole K-tiles, every
+  // K-outer operand's byte range from a split's first K-tile (two K-tiles of prefetch
+  // past its end included) addressable by a 32-bit offset, and a split-column A operand
+  // whose second block lies after the first in the same rows
+  bool buf = sizeof(T) == 2 && tt::opt(tt::OPT_GEMM_BUF) != 0 && g.K % (ttg::KTB / (int)sizeof(T)) == 0;
+  {
+    const long span = (long)(g.kt_per_split + 2) * (ttg::KTB / (int)sizeof(T)) * (long)sizeof(T);
+    if (akout && span * g.lda >= (1L << 32)) buf = false;
+    if (bkout && !shift && span * g.ldb >= (1L << 32)) buf = false;
+    if (!akout && (long)256 * g.lda * (long)sizeof(T) >= (1L << 31)) buf = false;
+    if (!bkout && (long)256 * g.ldb * (long)sizeof(T) >= (1L << 31)) buf = false;
+    for (int b = 0; b < 4 && g.a_split > 0; ++b) {
+      if (!g.a[b]) continue;
+      const long d = (long)((const char*)g.a_hi[b] - (const char*)g.a[b]) / (long)sizeof(T);
+      if (d < 0 || d + (g.M - g.a_split) > g.lda) buf = false;
+    }
+  }
   if (dma && persist_ok && (g.force_regstage == 0 || g.force_regstage >= 9) && g.splits == 1 && !g.beta && nk >= 2 && nk <= tt::opt(tt::OPT_GEMM_PERSIST_MAXK) && t256 >= 512 &&
       use_big(g.M, g.N, t256))
-    return launch_persist<T, TO>(akout, bkout, shift, g, (int)t256, st);
+    return launch_persist<T, TO>(akout, bkout, shift, g, (int)t256, buf, st);
   if (dma && g.force_regstage != 2 && use_big(g.M, g.N, t256)) {
+    if constexpr (sizeof(T) == 2)
+      if (tt::opt(tt::OPT_GEMM_A3) && buf)
+        return launch_t<T, TO, 256, 256, 2, 4, true, true, true>(akout, bkout, shift, g, t256, st);
     if (tt::opt(tt::OPT_GEMM_A3)) return launch_t<T, TO, 256, 256, 2, 4, true, true>(akout, bkout, shift, g, t256, st);
     return launch_t<T, TO, 256, 256, 2, 4, true>(akout, bkout, shift, g, t256, st);
   }

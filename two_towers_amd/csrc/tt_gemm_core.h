@@ -18,6 +18,8 @@
 // All images are XOR-swizzled so that the fragment reads are bank-conflict free
 // (verified against the gfx950 lane groups in tools/check_swizzle.py).
 #pragma once
+#include <type_traits>
+
 #include "tt_common.h"
 
 typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
@@ -334,6 +336,29 @@ TT_DEV void dma16(const void* src, uint32_t lds_addr) {
 TT_DEV uint32_t lds_addr_of(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
+// The same 16-byte-per-lane LDS-DMA through a buffer resource: per-lane byte offset voff
+// (fixed for a piece), wave-uniform soffset (the K-tile's byte advance, an SGPR), and
+// out-of-range offsets (past num_records) read zero. A piece issue is then scalar work
+// plus the load -- no per-lane select of the source and no 64-bit address add.
+typedef unsigned tt_rsrc4 __attribute__((ext_vector_type(4)));
+TT_DEV void dma16_buf(tt_rsrc4 rs, uint32_t voff, uint32_t soff, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rs), "s"(soff), "s"(lds_addr)
+      : "memory");
+}
+// raw buffer descriptor: 48-bit base, stride 0, num_records bytes, the flags of tt_rsrc
+TT_DEV tt_rsrc4 make_rsrc4(const void* base, uint32_t nrec) {
+  const uint64_t b = (uint64_t)(uintptr_t)base;
+  tt_rsrc4 r;
+  r.x = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  r.y = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32) & 0xFFFFu);
+  r.z = __builtin_amdgcn_readfirstlane(nrec);
+  r.w = 0x00020000u;
+  return r;
+}
 
 // Image of one K-tile of an operand with ROWS tile rows: K-contig = ROWS x 128 B rows;
 // K-outer = ROWS/128 sub-images of [KT k][128 columns] (16 KiB each).
@@ -455,7 +480,7 @@ struct DLoop {
 // CT: accumulate the transposed product (B fragment as the MFMA's first operand), so that
 // acc[i][j][r] is C(16i + (lane & 15), 16j + 4 (lane >> 4) + r): every lane holds 4
 // consecutive output columns of one row, which an epilogue stores straight from registers.
-template <typename T, bool AKO, bool BKO, bool BAL = false, bool A3 = false, bool CT = false>
+template <typename T, bool AKO, bool BKO, bool BAL = false, bool A3 = false, bool CT = false, bool BUF = false>
 struct Loop8 {
   static constexpr int HALF = 16384, SLOT = 4 * HALF, LDS_BYTES = A3 ? 10 * HALF : 2 * SLOT;
   static constexpr int BOFF = 6 * HALF;  // A3: first B slot
@@ -510,6 +535,12 @@ struct Loop8 {
   template <class L>
   TT_DEV static void issue_half(const L& ld, const Piece (&pc)[2], int r, long delta, uint32_t img) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if defined(TT_L8_DIAG) && TT_L8_DIAG == 1  // timing only (results wrong): no DMA in the loop
+    if (r > 1) return;
+#elif defined(TT_L8_DIAG) && TT_L8_DIAG == 2  // timing only: every K-tile re-reads the piece's first address
+    for (int j = 0; j < 2; ++j) dma16(pc[j].p, img + (uint32_t)(wave + 8 * j) * 1024u);
+    return;
+#endif
     int dt = 0;
     if constexpr (L::SHIFTED) dt = (int)(((long)r * KTE) % ld.T_);
 #pragma unroll
@@ -531,6 +562,81 @@ struct Loop8 {
       dma16(src, img + (uint32_t)(wave + 8 * j) * 1024u);
     }
   }
+  // BUF: the half-tile's two pieces through a buffer resource (dma16_buf): the resource
+  // and the per-K-tile byte advance are wave-uniform, each lane keeps one 32-bit offset
+  // per piece. Rows of a K-contig operand past its end and K-rows of a K-outer one past K
+  // read zero through num_records; columns past a K-outer operand's end and K-tiles past a
+  // split's end read whatever lies there, which only reaches output rows / columns that
+  // are never stored, or K-tiles that are never consumed. Needs K % KTE == 0 and the
+  // operand's byte range from the half's first K-tile below 2^32 (the host checks both).
+  struct BufHalf {
+    tt_rsrc4 rs;
+    uint32_t delta;
+    uint32_t voff[2];
+  };
+  template <bool KO, class L>
+  TT_DEV static void init_buf(const L& ld, int kt0, int K, int roff, BufHalf& h) {
+    constexpr int EPC = Elt<T>::EPC;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if constexpr (!KO) {
+      const long r0 = (long)ld.r0 + roff;
+      const long rows = (long)ld.rows - r0;
+      long nrec = rows > 0 ? rows * ld.ld * (long)sizeof(T) - (long)kt0 * KTB : 0;
+      nrec = nrec < 0 ? 0 : (nrec > 0xFFFFFFFFL ? 0xFFFFFFFFL : nrec);
+      h.rs = make_rsrc4(ld.base + r0 * ld.ld + (long)kt0 * KTE, (uint32_t)nrec);
+      h.delta = KTB;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int p = (wave + 8 * j) * 64 + lane;
+        const int row = p >> 3, c = (p & 7) ^ ((row >> 1) & 7);
+        h.voff[j] = (uint32_t)(((long)row * ld.ld + c * EPC) * (long)sizeof(T));
+      }
+    } else {
+      const long k0 = (long)kt0 * KTE;
+      long nrec = K > k0 ? ((long)K - k0) * ld.ld * (long)sizeof(T) : 0;
+      nrec = nrec > 0xFFFFFFFFL ? 0xFFFFFFFFL : nrec;
+      h.rs = make_rsrc4(ld.base + k0 * ld.ld, (uint32_t)nrec);
+      h.delta = (uint32_t)((long)KTE * ld.ld * (long)sizeof(T));
+      constexpr int CPR = 128 * (int)sizeof(T) / 16;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int p = (wave + 8 * j) * 64 + lane;
+        const int kl = p / CPR, q = p % CPR;
+        int c;
+        if constexpr (sizeof(T) == 2) c = q ^ (ko_v(kl) << 1);
+        else c = q ^ (((kl >> 2) & 1) << 2);
+        h.voff[j] = (uint32_t)(((long)kl * ld.ld + ld.col_off(roff + c * EPC)) * (long)sizeof(T));
+      }
+    }
+  }
+  TT_DEV static void issue_buf(const BufHalf& h, int r, uint32_t img) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)r * h.delta);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dma16_buf(h.rs, h.voff[j], soff, img + (uint32_t)(wave + 8 * j) * 1024u);
+  }
+  // One half-tile source: Piece form (any loader) or buffer form (BUF, plain loaders).
+  template <bool KO, class L>
+  struct PHalf {
+    L ld;
+    Piece pc[2];
+    long delta;
+    TT_DEV void init(const L& l, int kt0, int ktl, int K, int roff) {
+      ld = l;
+      init_half<KO>(l, kt0, ktl, K, roff, pc);
+      delta = KO ? (long)KTE * l.ld * (long)sizeof(T) : (long)KTB;
+    }
+    TT_DEV void issue(int r, uint32_t img) const { issue_half(ld, pc, r, delta, img); }
+  };
+  template <bool KO, class L>
+  struct BHalf {
+    BufHalf h;
+    TT_DEV void init(const L& l, int kt0, int ktl, int K, int roff) { init_buf<KO>(l, kt0, K, roff, h); }
+    TT_DEV void issue(int r, uint32_t img) const { issue_buf(h, r, img); }
+  };
+  template <bool KO, class L>
+  using Half = std::conditional_t<BUF && !L::SHIFTED && !L::KSPLIT, BHalf<KO, L>, PHalf<KO, L>>;
+
   TT_DEV static void quad(int mi, int ni, const uint4 (&fa)[2][4], const uint4 (&fb)[2][4], f32x4 (&acc)[TM][TN]) {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_s_setprio(1);
@@ -561,7 +667,13 @@ struct Loop8 {
     if constexpr (AKO) da = (long)KTE * la.ld * (long)sizeof(T);
     if constexpr (BKO) db = (long)KTE * lb.ld * (long)sizeof(T);
     if constexpr (A3) {
-      run3(la, lb, kt1 - kt0, lds, base, da, db, pa0, pa1, pb0, pb1, acc);
+      Half<AKO, LA> ha0, ha1;
+      Half<BKO, LB> hb0, hb1;
+      ha0.init(la, kt0, kt1, K, 0);
+      ha1.init(la, kt0, kt1, K, 128);
+      hb0.init(lb, kt0, kt1, K, 0);
+      hb1.init(lb, kt0, kt1, K, 128);
+      run3(kt1 - kt0, lds, base, ha0, ha1, hb0, hb1, acc);
       return;
     }
     issue_half(la, pa0, 0, da, base);
@@ -644,20 +756,19 @@ struct Loop8 {
   // columns 0-31 and restages A0 of r+2, P2 reads B columns 32-63 and restages A1 of r+2,
   // P3 reads A rows 64-127, P4 restages both B halves of r+2 into B's current slot and
   // waits for K-tile r+1 with the 8 youngest DMAs (A and B of r+2) still in flight.
-  template <class LA, class LB>
-  TT_DEV static void run3(const LA& la, const LB& lb, int nk, char* lds, uint32_t base, long da, long db,
-                          const Piece (&pa0)[2], const Piece (&pa1)[2], const Piece (&pb0)[2], const Piece (&pb1)[2],
+  template <class HA, class HB>
+  TT_DEV static void run3(int nk, char* lds, uint32_t base, const HA& pa0, const HA& pa1, const HB& pb0, const HB& pb1,
                           f32x4 (&acc)[TM][TN]) {
     const int wave = threadIdx.x >> 6;
     const int wr = wave >> 2, bh = (wave & 3) >> 1, bc = (wave & 1) * 64;
-    issue_half(la, pa0, 0, da, base);
-    issue_half(la, pa1, 0, da, base + HALF);
-    issue_half(lb, pb0, 0, db, base + BOFF);
-    issue_half(lb, pb1, 0, db, base + BOFF + HALF);
-    issue_half(la, pa0, 1, da, base + 2 * HALF);
-    issue_half(la, pa1, 1, da, base + 3 * HALF);
-    issue_half(lb, pb0, 1, db, base + BOFF + 2 * HALF);
-    issue_half(lb, pb1, 1, db, base + BOFF + 3 * HALF);
+    pa0.issue(0, base);
+    pa1.issue(0, base + HALF);
+    pb0.issue(0, base + BOFF);
+    pb1.issue(0, base + BOFF + HALF);
+    pa0.issue(1, base + 2 * HALF);
+    pa1.issue(1, base + 3 * HALF);
+    pb0.issue(1, base + BOFF + 2 * HALF);
+    pb1.issue(1, base + BOFF + 3 * HALF);
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     const bool late = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;  // wave row 1
@@ -677,21 +788,21 @@ struct Loop8 {
 #pragma unroll
         for (int j = 0; j < 2; ++j) fb[ks][j] = frag2<T, BKO>(ib, bc + 16 * j, ks);
       }
-      issue_half(la, pa0, r + 2, da, anx);
+      pa0.issue(r + 2, anx);
       quad(0, 0, fa, fb, acc);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int j = 2; j < 4; ++j) fb[ks][j] = frag2<T, BKO>(ib, bc + 16 * j, ks);
-      issue_half(la, pa1, r + 2, da, anx + HALF);
+      pa1.issue(r + 2, anx + HALF);
       quad(0, 1, fa, fb, acc);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int i = 0; i < 4; ++i) fa[ks][i] = frag2<T, AKO>(ia, 64 + 16 * i, ks);
       quad(1, 1, fa, fb, acc);
-      issue_half(lb, pb0, r + 2, db, bcur);
-      issue_half(lb, pb1, r + 2, db, bcur + HALF);
+      pb0.issue(r + 2, bcur);
+      pb1.issue(r + 2, bcur + HALF);
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       quad(1, 0, fa, fb, acc);
       as = as == 2 ? 0 : as + 1;
@@ -746,6 +857,12 @@ struct KOPlain {  // columns [c0, c0+128) of a row-major [K][ld] matrix
     return gc < csplit ? base + k * ld + gc : base1 + k * ld + (gc - csplit);
   }
   TT_DEV const T* at(long k, int col) const { return raw_at(k, col); }
+  // element offset of tile column col from base (k = 0): the buffer form of raw_at; base1
+  // must lie in the same rows (same ld) at or after base
+  TT_DEV long col_off(int col) const {
+    const int gc = c0 + col;
+    return gc < csplit ? (long)gc : (long)(base1 - base) + (gc - csplit);
+  }
 };
 // K-outer operand whose k index is (b*T + t) and whose source row is (b*T + t + shift),
 // zero when t+shift falls outside [0,T). Used for the GRU h_{s-1} operand of dW_hh.

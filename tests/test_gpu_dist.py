@@ -310,7 +310,8 @@ def _bench_scale_rank(port, use_pg, out):
         opt.step()
         tta.check_gru_status()
         out.put((float(loss.detach()), {k: v.detach().cpu().float().numpy().copy() for k, v in m.state_dict().items()},
-                 crit.last_indices.cpu().numpy().copy()))
+                 crit.last_indices.cpu().numpy().copy(),
+                 {k: p.grad.detach().cpu().float().numpy().copy() for k, p in m.named_parameters()}))
     finally:
         if use_pg:
             torch.distributed.destroy_process_group()
@@ -331,15 +332,19 @@ def test_rccl_one_rank_bench_scale_step_is_bit_identical():
         res.append(out.get(timeout=240))
         p.join(timeout=60)
         assert p.exitcode == 0
-    (l0, w0, i0), (l1, w1, i1) = res
+    (l0, w0, i0, g0), (l1, w1, i1, g1) = res
     assert l0 == l1, (l0, l1)
     assert (i0 == i1).all()
     for k in w0:
         if k.startswith("query_"):
             assert np.array_equal(w0[k], w1[k]), k
+    for k in g0:
+        if k.startswith("query_"):
+            assert np.array_equal(g0[k], g1[k]), k
         else:
             # the margin backward sums each document's gradient with float atomics
-            # (tt_loss.hip margin_ddn_kernel), so the doc tower's gradients -- and after
-            # Adam (update ~ lr * g / (|g| + eps)) its weights -- differ between ANY two runs
-            # at rounding level, process group or not
-            assert float(np.abs(w0[k] - w1[k]).max()) <= 1e-6, k
+            # (tt_loss.hip margin_ddn_kernel), so the doc tower's gradients differ between
+            # ANY two runs at rounding level, process group or not (and so do its weights
+            # after Adam, whose first update is ~ lr * sign(g) wherever |g| >> eps)
+            scale = float(np.abs(g0[k]).max()) + 1e-30
+            assert float(np.abs(g0[k] - g1[k]).max()) <= 1e-3 * scale, (k, float(np.abs(g0[k] - g1[k]).max()), scale)

@@ -74,7 +74,7 @@ def test_buffer_dma_split_k_wgrad_hh_composition():
     for d in range(2):
         assert torch.equal(c0[d], c1[d]), d
         dgh = torch.cat([a[d][:, :2 * H], a_hi[d][:, :H]], 1).float()
-        h = b[d].float().view(Bsz, T, H)
+        h = b[d][:, :H].float().reshape(Bsz, T, H)
         hs = torch.zeros_like(h)
         if d == 0:
             hs[:, 1:] = h[:, :-1]

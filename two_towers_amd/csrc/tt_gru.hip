@@ -584,6 +584,9 @@ TT_DEV void wait_younger(int n) {  // s_waitcnt vmcnt(P * n), n in [0, N]
   }
 }
 
+#ifndef TT_BWD_BUF  // gru_bwd_rows product DMAs through buffer resources (0: per-lane pointers)
+#define TT_BWD_BUF 1
+#endif
 template <int H>
 __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
   using C = BwdRowsCfg<H>;
@@ -654,6 +657,32 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
 #pragma unroll
       for (int j = 0; j < C::NCB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (!last && !(dbg & 1)) {
+#if TT_BWD_BUF
+      // the pieces through buffer resources (ttg::dma16_buf): A = the tile's rows at time tn,
+      // r|z columns from dgx (k < 2H) or the n column block from dgh (k >= 2H, the resource
+      // based 2H columns early so that k indexes it directly), rows past B read zero; W_hh
+      // from the pass's first unit; the K-tile advance is the SGPR soffset
+      const long abytes = (long)(a.B - m0) * ldr * 2;
+      const uint32_t anrec = (uint32_t)(abytes > 0xFFFFFFFFL ? 0xFFFFFFFFL : abytes);
+      const ttg::tt_rsrc4 rsx = ttg::make_rsrc4(DGX + (long)tn * a.ldd + (long)m0 * ldr, anrec);
+      const ttg::tt_rsrc4 rsh = ttg::make_rsrc4(DGH + (long)tn * a.ldd + (long)m0 * ldr - 2 * H, anrec);
+      const ttg::tt_rsrc4 rsw = ttg::make_rsrc4(W + u0, 0xFFFFFFFFu);
+      uint32_t voff[C::P];
+#pragma unroll
+      for (int j = 0; j < C::P; ++j)
+        voff[j] = prow[j] >= 0 ? (uint32_t)(((long)prow[j] * ldr + pcol[j]) * 2) : (uint32_t)(pcol[j] * 2);
+      auto issue = [&](int r) {
+        const uint32_t img = lbase + (uint32_t)(r % C::NS) * C::SLOT;
+        const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const bool hi = r * 32 >= 2 * H;
+#pragma unroll
+        for (int j = 0; j < C::P; ++j) {
+          const int pc = wv + 8 * j;
+          if (pc < 8) ttg::dma16_buf(hi ? rsh : rsx, voff[j], (uint32_t)r * 64u, img + (uint32_t)pc * 1024u);
+          else ttg::dma16_buf(rsw, voff[j], (uint32_t)r * (uint32_t)(64 * H), img + (uint32_t)pc * 1024u);
+        }
+      };
+#else
       // A source of this lane's A pieces: dL/dgh_{s+1} of row m0 + prow, r|z from dgx, n from dgh
       const char* as0[C::P];
       const char* as1[C::P];
@@ -681,6 +710,7 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
           ttg::dma16(src, img + (uint32_t)pc * 1024u);
         }
       };
+#endif
       issue(0);
       issue(1);
       issue(2);

@@ -658,30 +658,22 @@ struct Loop8 {
     const int wave = threadIdx.x >> 6;
     const int wr = wave >> 2, bh = (wave & 3) >> 1, bc = (wave & 1) * 64;
     const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr_of(lds));
-    Piece pa0[2], pa1[2], pb0[2], pb1[2];
-    init_half<AKO>(la, kt0, kt1, K, 0, pa0);
-    init_half<AKO>(la, kt0, kt1, K, 128, pa1);
-    init_half<BKO>(lb, kt0, kt1, K, 0, pb0);
-    init_half<BKO>(lb, kt0, kt1, K, 128, pb1);
-    long da = KTB, db = KTB;  // K-contig operands advance 128 B per K-tile
-    if constexpr (AKO) da = (long)KTE * la.ld * (long)sizeof(T);
-    if constexpr (BKO) db = (long)KTE * lb.ld * (long)sizeof(T);
+    Half<AKO, LA> pa0, pa1;
+    Half<BKO, LB> pb0, pb1;
+    pa0.init(la, kt0, kt1, K, 0);
+    pa1.init(la, kt0, kt1, K, 128);
+    pb0.init(lb, kt0, kt1, K, 0);
+    pb1.init(lb, kt0, kt1, K, 128);
     if constexpr (A3) {
-      Half<AKO, LA> ha0, ha1;
-      Half<BKO, LB> hb0, hb1;
-      ha0.init(la, kt0, kt1, K, 0);
-      ha1.init(la, kt0, kt1, K, 128);
-      hb0.init(lb, kt0, kt1, K, 0);
-      hb1.init(lb, kt0, kt1, K, 128);
-      run3(kt1 - kt0, lds, base, ha0, ha1, hb0, hb1, acc);
+      run3(kt1 - kt0, lds, base, pa0, pa1, pb0, pb1, acc);
       return;
     }
-    issue_half(la, pa0, 0, da, base);
-    issue_half(la, pa1, 0, da, base + HALF);
-    issue_half(lb, pb0, 0, db, base + 2 * HALF);
-    issue_half(lb, pb1, 0, db, base + 3 * HALF);
-    issue_half(lb, pb0, 1, db, base + SLOT + 2 * HALF);
-    issue_half(lb, pb1, 1, db, base + SLOT + 3 * HALF);
+    pa0.issue(0, base);
+    pa1.issue(0, base + HALF);
+    pb0.issue(0, base + 2 * HALF);
+    pb1.issue(0, base + 3 * HALF);
+    pb0.issue(1, base + SLOT + 2 * HALF);
+    pb1.issue(1, base + SLOT + 3 * HALF);
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     const bool late = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;  // wave row 1
@@ -703,21 +695,21 @@ struct Loop8 {
 #pragma unroll
           for (int j = 0; j < 2; ++j) fb[ks][j] = frag2<T, BKO>(ib, bc + 16 * j, ks);
         }
-        issue_half(la, pa0, r + 1, da, nxt);
+        pa0.issue(r + 1, nxt);
         quad(0, 0, fa, fb, acc);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
           for (int j = 2; j < 4; ++j) fb[ks][j] = frag2<T, BKO>(ib, bc + 16 * j, ks);
-        issue_half(la, pa1, r + 1, da, nxt + HALF);
+        pa1.issue(r + 1, nxt + HALF);
         quad(0, 1, fa, fb, acc);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
           for (int i = 0; i < 4; ++i) fa[ks][i] = frag2<T, AKO>(ia, 64 + 16 * i, ks);
         quad(1, 1, fa, fb, acc);
-        issue_half(lb, pb0, r + 2, db, cur + 2 * HALF);
-        issue_half(lb, pb1, r + 2, db, cur + 3 * HALF);
+        pb0.issue(r + 2, cur + 2 * HALF);
+        pb1.issue(r + 2, cur + 3 * HALF);
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         quad(1, 0, fa, fb, acc);
         continue;
@@ -730,20 +722,20 @@ struct Loop8 {
 #pragma unroll
         for (int j = 0; j < 4; ++j) fb[ks][j] = frag2<T, BKO>(ib, bc + 16 * j, ks);
       }
-      issue_half(la, pa0, r + 1, da, nxt);
+      pa0.issue(r + 1, nxt);
       quad(0, 0, fa, fb, acc);
       // P2
-      issue_half(la, pa1, r + 1, da, nxt + HALF);
+      pa1.issue(r + 1, nxt + HALF);
       quad(0, 1, fa, fb, acc);
       // P3
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int i = 0; i < 4; ++i) fa[ks][i] = frag2<T, AKO>(ia, 64 + 16 * i, ks);
-      issue_half(lb, pb0, r + 2, db, cur + 2 * HALF);
+      pb0.issue(r + 2, cur + 2 * HALF);
       quad(1, 1, fa, fb, acc);
       // P4
-      issue_half(lb, pb1, r + 2, db, cur + 3 * HALF);
+      pb1.issue(r + 2, cur + 3 * HALF);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       quad(1, 0, fa, fb, acc);
     }

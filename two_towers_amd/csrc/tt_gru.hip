@@ -355,6 +355,13 @@ TT_DEV void unpack8(uint4 v, float (&f)[8]) {
   f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xFFFF0000u);
 }
 
+#ifndef TT_BWD_BUF  // backward product DMAs through buffer resources (0: per-lane pointers)
+#define TT_BWD_BUF 1
+#endif
+#ifndef TT_BWD_CREG  // gru_bwd_rows: the BPTT carry in registers (0: bf16 ping-pong buffer in HBM)
+#define TT_BWD_CREG 1
+#endif
+
 // ---- backward step on 256x256 tiles (bf16): the recurrent GEMM on the 8-phase loop --
 // One workgroup (8 waves) per 256 rows x 256 hidden units of a recurrence: at B 8192,
 // H 512 the four recurrences are exactly 256 tiles, one per CU, so the GEMM runs at the
@@ -363,7 +370,7 @@ TT_DEV void unpack8(uint4 v, float (&f)[8]) {
 // gradients. Bias partials land in partial row 2*mt (tt_gru_bias_rows() counts 128-row
 // tiles; the odd rows stay zero).
 __global__ __launch_bounds__(512) void gru_bwd_big(BwdArgs a) {
-  using L8 = ttg::Loop8<bf16_t, false, true>;
+  using L8 = ttg::Loop8<bf16_t, false, true, false, false, false, TT_BWD_BUF != 0>;  // W_hh by buffer DMA
   static_assert(L8::LDS_BYTES >= 128 * 256 * 4 && L8::LDS_BYTES >= 8 * 4 * 256 * 4, "staging fits the slots");
   __shared__ __attribute__((aligned(16))) char lds[L8::LDS_BYTES];
   const int H = a.H, T_ = a.T, s = a.s;
@@ -584,9 +591,6 @@ TT_DEV void wait_younger(int n) {  // s_waitcnt vmcnt(P * n), n in [0, N]
   }
 }
 
-#ifndef TT_BWD_BUF  // gru_bwd_rows product DMAs through buffer resources (0: per-lane pointers)
-#define TT_BWD_BUF 1
-#endif
 template <int H>
 __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
   using C = BwdRowsCfg<H>;
@@ -644,6 +648,16 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
   constexpr int dbg = 0;
 #endif
 
+  // CREG: the BPTT carry dh_s * z_s never leaves the chip. The epilogue writes it (bf16, the
+  // rounding of the carry buffer it replaces) over the slot of the accumulator image it has
+  // just read for the same (row, units), and the next step's product starts from it: each
+  // lane loads its accumulator tile from that image before the first DMA of the step, so
+  // the product sums onto the carry (dh = bf16(carry + dL/dgh W_hh) + dy, where the
+  // buffer form adds the carry after rounding the product). Saves the carry's 4 of the
+  // ~28 bytes per row, unit and step.
+  constexpr bool CREG = TT_BWD_CREG != 0 && C::NP == 1;
+  constexpr int NIT = 128 / C::RPI;  // epilogue row iterations per thread
+  static_assert(!CREG || 128 * C::LDB * 2 + C::RPI * C::HP * 4 <= C::LDS, "carry image + one bias row of partials");
   for (int s = T_ - 1; s >= 0; --s) {
     const int t = R.dir ? T_ - 1 - s : s;
     const int tn = R.dir ? t - 1 : t + 1;
@@ -656,6 +670,21 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < C::NCB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (CREG && !last) {
+      // this lane's accumulator tile <- the carry image (C^T layout: 4 consecutive units of
+      // one row), then every lane must be done reading before the first DMA overwrites it
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jc = 0; jc < C::NCB; ++jc) {
+          const uint2 w = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(lds) +
+                                                          (wr * 64 + 16 * i + (lane & 15)) * C::LDB + wc * (C::HP / 4) +
+                                                          16 * jc + 4 * (lane >> 4));
+          acc[i][jc] = f32x4{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xFFFF0000u),
+                             __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xFFFF0000u)};
+        }
+      __syncthreads();
+    }
     if (!last && !(dbg & 1)) {
 #if TT_BWD_BUF
       // the pieces through buffer resources (ttg::dma16_buf): A = the tile's rows at time tn,
@@ -768,8 +797,7 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) bsum[q][e] = 0.f;
     constexpr int NB = 2;
-#pragma unroll 1
-    for (int kb = 0; kb < 128 / C::RPI; kb += NB) {
+    auto batch = [&](const int kb) {
       uint4 vin[NB][7];
 #pragma unroll
       for (int kk = 0; kk < NB; ++kk) {
@@ -778,7 +806,7 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
         const uint32_t oc = ok ? (uint32_t)(bl * H + u0 + jg) * 2u : 0x80000000u;
         const uint32_t oy = ok ? (uint32_t)(bl * T_ * (int)a.ldy + u0 + jg) * 2u : 0x80000000u;
         const uint32_t os = ok ? (uint32_t)(bl * T_ * 4 * H + u0 + jg) * 2u : 0x80000000u;
-        vin[kk][0] = ld16_buf(rc, oc, 0);
+        vin[kk][0] = CREG ? make_uint4(0, 0, 0, 0) : ld16_buf(rc, oc, 0);  // CREG: the carry is in gm
         vin[kk][1] = ld16_buf(rd, oy, 0);
 #pragma unroll
         for (int q = 0; q < 4; ++q) vin[kk][2 + q] = ld16_buf(rsv, os, q * 2 * H);
@@ -814,11 +842,13 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
           cout[e] = dht * zg;
           bsum[0][e] += drp; bsum[1][e] += dzp; bsum[2][e] += dnp; bsum[3][e] += dnp * rg;
         }
+        if constexpr (CREG)  // over the gm slot this thread just read: the next step's carry
+          *reinterpret_cast<uint4*>(L16 + ((bl * C::LDB + jg) >> 1)) = pack8bf(cout);
         if (dbg & 4) {
           if (o_r[0] == 12345.f) L16[0] = __float_as_uint(o_z[1] + o_n[2] + o_hn[3] + cout[4]);
           continue;
         }
-        st8(cr_cur + (long)bl * H + u0 + jg, cout);
+        if constexpr (!CREG) st8(cr_cur + (long)bl * H + u0 + jg, cout);
         const long row = (long)b * T_ + t;
         bf16_t* xw = DGXw + row * a.ldd + u0 + jg;
         st8(xw, o_r);
@@ -826,19 +856,39 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
         st8_sc1(grs, (int)(((long)bl * T_ * a.ldd + u0 + jg + 2 * H) * 2L), o_n, (bf16_t*)nullptr);
         st8(DGHw + row * a.ldd + u0 + jg, o_hn);
       }
-    }
+    };
+#pragma unroll 1
+    for (int kb = 0; kb < NIT; kb += NB) batch(kb);
     __syncthreads();
-    float* red = L;
+    if constexpr (CREG) {
+      // the bias partials one gate row at a time, past the carry image
+      float* red = reinterpret_cast<float*>(lds + 128 * C::LDB * 2);
+#pragma unroll 1
+      for (int q = 0; q < 4; ++q) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+        for (int e = 0; e < 8; ++e) red[rsub * C::HP + jg + e] = bsum[q][e];
+        __syncthreads();
+        for (int c = tid; c < C::HP; c += 512) {
+          float v = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) red[(rsub * 4 + q) * C::HP + jg + e] = bsum[q][e];
-    __syncthreads();
-    for (int c = tid; c < 4 * C::HP; c += 512) {
-      float v = 0.f;
+          for (int w = 0; w < C::RPI; ++w) v += red[w * C::HP + c];
+          part[q * H + u0 + c] += v;
+        }
+        __syncthreads();
+      }
+    } else {
+      float* red = L;
 #pragma unroll
-      for (int w = 0; w < C::RPI; ++w) v += red[w * 4 * C::HP + c];
-      part[(c / C::HP) * H + u0 + c % C::HP] += v;
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[(rsub * 4 + q) * C::HP + jg + e] = bsum[q][e];
+      __syncthreads();
+      for (int c = tid; c < 4 * C::HP; c += 512) {
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < C::RPI; ++w) v += red[w * 4 * C::HP + c];
+        part[(c / C::HP) * H + u0 + c % C::HP] += v;
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

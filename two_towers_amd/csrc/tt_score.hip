@@ -41,8 +41,8 @@ constexpr int SC_COLS = 64;     // document columns per tile (= per chunk)
 #ifndef HN_W4
 #define HN_W4 1
 #endif
-#ifndef HN_PIPE_Q  // query prologue overlapped with the first tile (0: retired up front, round-4 form)
-#define HN_PIPE_Q 1
+#ifndef HN_PIPE_Q  // 1: query prologue overlapped with the first tile (measured no faster: profiles/r04_hn_scan_pipeq_h.txt)
+#define HN_PIPE_Q 0
 #endif
 constexpr int SC_TPS_MAX = 32;  // tiles per workgroup (chunk-max staging)
 

@@ -358,6 +358,9 @@ TT_DEV void unpack8(uint4 v, float (&f)[8]) {
 #ifndef TT_BWD_BUF  // backward product DMAs through buffer resources (0: per-lane pointers)
 #define TT_BWD_BUF 1
 #endif
+#ifndef TT_BWD_NT
+#define TT_BWD_NT 0
+#endif
 #ifndef TT_BWD_CREG  // gru_bwd_rows: the BPTT carry in registers (0: bf16 ping-pong buffer in HBM)
 #define TT_BWD_CREG 1
 #endif
@@ -461,10 +464,12 @@ __global__ __launch_bounds__(512) void gru_bwd_big(BwdArgs a) {
         const uint32_t oy = ok ? (uint32_t)(bl * T_ * (int)a.ldy + j) * 2u : 0x80000000u;
         const uint32_t os = ok ? (uint32_t)(bl * T_ * (int)S4 + j) * 2u : 0x80000000u;
         vin[kk][0] = ld16_buf(rc, oc, 0);
-        vin[kk][1] = ld16_buf(rd, oy, 0);
+        // TT_BWD_NT: non-temporal loads of the once-read streams (1: S, 2: dy and h_{s-1}), so
+        // that they do not displace the re-read gate gradients from the caches
+        vin[kk][1] = ld16_buf<(TT_BWD_NT & 2) ? 2 : 0>(rd, oy, 0);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) vin[kk][2 + q] = ld16_buf(rsv, os, q * 2 * H);
-        vin[kk][6] = ld16_buf(ry, oy, 0);
+        for (int q = 0; q < 4; ++q) vin[kk][2 + q] = ld16_buf<(TT_BWD_NT & 1) ? 2 : 0>(rsv, os, q * 2 * H);
+        vin[kk][6] = ld16_buf<(TT_BWD_NT & 2) ? 2 : 0>(ry, oy, 0);
       }
 #pragma unroll
       for (int kk = 0; kk < NB; ++kk) {
@@ -807,10 +812,12 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
         const uint32_t oy = ok ? (uint32_t)(bl * T_ * (int)a.ldy + u0 + jg) * 2u : 0x80000000u;
         const uint32_t os = ok ? (uint32_t)(bl * T_ * 4 * H + u0 + jg) * 2u : 0x80000000u;
         vin[kk][0] = CREG ? make_uint4(0, 0, 0, 0) : ld16_buf(rc, oc, 0);  // CREG: the carry is in gm
-        vin[kk][1] = ld16_buf(rd, oy, 0);
+        // TT_BWD_NT: non-temporal loads of the once-read streams (1: S, 2: dy and h_{s-1}), so
+        // that they do not displace the re-read gate gradients from the caches
+        vin[kk][1] = ld16_buf<(TT_BWD_NT & 2) ? 2 : 0>(rd, oy, 0);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) vin[kk][2 + q] = ld16_buf(rsv, os, q * 2 * H);
-        vin[kk][6] = ld16_buf(ry, oy, 0);
+        for (int q = 0; q < 4; ++q) vin[kk][2 + q] = ld16_buf<(TT_BWD_NT & 1) ? 2 : 0>(rsv, os, q * 2 * H);
+        vin[kk][6] = ld16_buf<(TT_BWD_NT & 2) ? 2 : 0>(ry, oy, 0);
       }
 #pragma unroll
       for (int kk = 0; kk < NB; ++kk) {

@@ -359,7 +359,7 @@ TT_DEV void unpack8(uint4 v, float (&f)[8]) {
 #define TT_BWD_BUF 1
 #endif
 #ifndef TT_BWD_NT
-#define TT_BWD_NT 0
+#define TT_BWD_NT 3
 #endif
 #ifndef TT_BWD_CREG  // gru_bwd_rows: the BPTT carry in registers (0: bf16 ping-pong buffer in HBM)
 #define TT_BWD_CREG 1
@@ -1864,7 +1864,10 @@ static int gru_fwd_xc_launch(const FwdArgs& a, int nrec, int B, int T, int H, lo
   const void* fn = H == 512 ? (drop ? xc_kernel<512, true>() : xc_kernel<512, false>())
                             : (drop ? xc_kernel<256, true>() : xc_kernel<256, false>());
   // cooperative: the runtime checks the grid against the co-residency limit at launch
-  const hipError_t e = hipLaunchCooperativeKernel(fn, dim3(g.grid), dim3(xc::NT), args, 0, st);
+  // (option gru_xc_coop 0: a plain launch, guarded by xc_plan's occupancy check only)
+  const hipError_t e = tt::opt(tt::OPT_GRU_XC_COOP)
+                           ? hipLaunchCooperativeKernel(fn, dim3(g.grid), dim3(xc::NT), args, 0, st)
+                           : hipLaunchKernel(fn, dim3(g.grid), dim3(xc::NT), args, 0, st);
   if (e == hipErrorCooperativeLaunchTooLarge) {
     (void)hipGetLastError();  // clear it: the row-owning kernel runs instead
     return 0;

@@ -176,6 +176,9 @@ int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B, int T, in
 /* Kernel launches tt_gru_bwd issues: 1 for the row-owning bf16 kernel (H 256 or 512: one
  * workgroup per 128 batch rows x all H units walks every step), T otherwise. */
 int tt_gru_bwd_launches(int dtype, int T, int H);
+/* 1 when tt_gru_bwd keeps the BPTT carry on chip (the row-owning kernel at H <= 512: no
+ * carry bytes in HBM), 0 when it round-trips a bf16 / fp32 carry buffer (dhstate). */
+int tt_gru_bwd_carry_on_chip(int dtype, int T, int H);
 int tt_gru_bias_rows(int B);
 
 /* ------------------------------------------------------------ projection head */

@@ -111,6 +111,7 @@ _SIGS = {
                            c_void_p]),
     "tt_gru_bias_rows": (c_int, [c_int]),
     "tt_gru_bwd_launches": (c_int, [c_int, c_int, c_int]),
+    "tt_gru_bwd_carry_on_chip": (c_int, [c_int, c_int, c_int]),
     "tt_gru_fwd_launches": (c_int, [c_int, c_int, c_int]),
     "tt_gru_fwd_ws_size": (c_long, [c_int, c_int, c_int, c_int, c_int, c_long, c_long]),
     "tt_gru_fwd_launches_for": (c_int, [c_int, c_int, c_int, c_int, c_int, c_long, c_long]),

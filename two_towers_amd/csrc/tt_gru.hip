@@ -1709,6 +1709,10 @@ static bool gru_bwd_persistent(int dtype, int H) {
          tt::opt(tt::OPT_GRU_BWD_ROWS) != 64 && o != 0;
 }
 extern "C" int tt_gru_bwd_launches(int dtype, int T, int H) { return gru_bwd_persistent(dtype, H) ? 1 : T; }
+extern "C" int tt_gru_bwd_carry_on_chip(int dtype, int T, int H) {
+  (void)T;
+  return TT_BWD_CREG != 0 && gru_bwd_persistent(dtype, H) && H <= 512 ? 1 : 0;
+}
 
 // Per-device side stream + fork/join events for tt_gru_bwd's second launch chain,
 // created once per device under a mutex (host threads may call on distinct streams).

@@ -284,11 +284,12 @@ def _gru_layer_bwd(cfg, layer, B, T, S, Y, dY, dfinal, packs):
             r.dir = d
     ldf = dfinal[0].shape[1] if dfinal is not None else 0
     # algorithmic bytes per (row, unit): saved 4 + h_{s-1} 1 (+ dY 1) + dgh_{s+1} 3 (GEMM
-    # operand) + 4 written gradients (r, z, n, W_hn h) + the carry read and written, all
-    # of dt
+    # operand) + 4 written gradients (r, z, n, W_hn h) + the carry read and written (unless
+    # the kernel keeps it on chip), all of dt
     esz = 2 if dt == torch.bfloat16 else 4
     nl = lib.tt_gru_bwd_launches(dtype_code(dt), T, H)
-    per = esz * (14 + (1 if dY is not None else 0))
+    carry = 0 if lib.tt_gru_bwd_carry_on_chip(dtype_code(dt), T, H) else 2
+    per = esz * (12 + carry + (1 if dY is not None else 0))
     kname = (f"gru_bwd_rows<{H}>" if nl == 1 else
              "gru_bwd_big" if dt == torch.bfloat16 and H % 256 == 0 and _lib.get_option("gru_bwd_big") else "gru_bwd_step<")
     with timing.region("gru_bwd", nl, 2.0 * B * 3 * H * H * 2 * n * (T - 1), float(B * T * H * 2 * n * per),

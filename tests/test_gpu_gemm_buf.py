@@ -27,29 +27,32 @@ def _rel(a, b):
     return float((a.double() - b.double()).abs().max() / (b.double().abs().max() + 1e-12))
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("akout,bkout", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("path", ["persist", "long_k"])
-def test_buffer_dma_gemm_is_bit_identical(akout, bkout, path):
-    # persist: >= 512 tiles of 256^2 at 16 K-tiles; long_k: 32 K-tiles (past the persistent cap)
-    m, n, k = (8200, 4136, 1024) if path == "persist" else (4200, 4136, 2048)
+def test_buffer_dma_gemm_is_bit_identical(akout, bkout, path, dt):
+    # persist: >= 512 tiles of 256^2 at <= 24 K-tiles; long_k: past the persistent cap
+    if dt == torch.bfloat16:
+        m, n, k = (8200, 4136, 1024) if path == "persist" else (4200, 4136, 2048)
+    else:  # fp32 K-tiles are 32 deep
+        m, n, k = (8200, 4136, 512) if path == "persist" else (4200, 4136, 1024)
     g = torch.Generator().manual_seed(31 + 2 * akout + bkout)
-    A = torch.randn(m, k, generator=g).to(torch.bfloat16)
-    B = torch.randn(n, k, generator=g).to(torch.bfloat16)
+    A = torch.randn(m, k, generator=g).to(dt)
+    B = torch.randn(n, k, generator=g).to(dt)
     bias = torch.randn(n, generator=g).to(DEV)
     Ad = (A.t().contiguous() if akout else A).to(DEV)
     Bd = (B.t().contiguous() if bkout else B).to(DEV)
 
     def run():
-        C = torch.empty(m, n, device=DEV, dtype=torch.bfloat16)
+        C = torch.empty(m, n, device=DEV, dtype=dt)
         ops.gemm([Ad], [Bd], [C], m=m, n=n, k=k, lda=m if akout else k, ldb=n if bkout else k, ldc=n,
-                 a_kouter=bool(akout), b_kouter=bool(bkout), dtype=torch.bfloat16, out_dtype=torch.bfloat16,
-                 bias=[bias], splits=1)
+                 a_kouter=bool(akout), b_kouter=bool(bkout), dtype=dt, out_dtype=dt, bias=[bias], splits=1)
         return C
 
     c0, c1 = _both(run)
     assert torch.equal(c0, c1)
-    ref = A.to(DEV).float() @ B.to(DEV).float().t() + bias
-    assert _rel(c1.float(), ref) < 1e-2
+    ref = A.to(DEV).double() @ B.to(DEV).double().t() + bias.double()
+    assert _rel(c1.double(), ref) < (1e-2 if dt == torch.bfloat16 else 1e-5)
 
 
 def test_buffer_dma_split_k_wgrad_hh_composition():

@@ -855,7 +855,7 @@ int launch_persist(int akout, int bkout, bool shift, const GemmArgs& g, int ntil
   hipLaunchKernelGGL((gemm_persist<T, AK, BK, SH, TO, A3, BUF>), grid, blk, 0, st, g, ntiles)
 #define TT_L2(AK, BK, SH) \
   do {                     \
-    if (a3 && buf) TT_L(AK, BK, SH, true, sizeof(T) == 2); \
+    if (a3 && buf) TT_L(AK, BK, SH, true, true); \
     else if (a3) TT_L(AK, BK, SH, true, false); \
     else TT_L(AK, BK, SH, false, false);   \
   } while (0)
@@ -919,11 +919,11 @@ int launch_gemm(int akout, int bkout, bool shift, GemmArgs& g, int nbatch, hipSt
   // slower at 48 and 128), no split-K, no accumulate (env TT_GEMM_PERSIST=0 disables)
   const bool persist_ok = tt::opt(tt::OPT_GEMM_PERSIST) != 0;
   const int nk = (g.K * (int)sizeof(T) + ttg::KTB - 1) / ttg::KTB;
-  // operand DMAs through buffer resources (Loop8 BUF): bf16, whole K-tiles, every
+  // operand DMAs through buffer resources (Loop8 BUF): whole K-tiles, every
   // K-outer operand's byte range from a split's first K-tile (two K-tiles of prefetch
   // past its end included) addressable by a 32-bit offset, and a split-column A operand
   // whose second block lies after the first in the same rows
-  bool buf = sizeof(T) == 2 && tt::opt(tt::OPT_GEMM_BUF) != 0 && g.K % (ttg::KTB / (int)sizeof(T)) == 0;
+  bool buf = tt::opt(tt::OPT_GEMM_BUF) != 0 && g.K % (ttg::KTB / (int)sizeof(T)) == 0;
   {
     const long span = (long)(g.kt_per_split + 2) * (ttg::KTB / (int)sizeof(T)) * (long)sizeof(T);
     if (akout && span * g.lda >= (1L << 32)) buf = false;
@@ -940,9 +940,8 @@ int launch_gemm(int akout, int bkout, bool shift, GemmArgs& g, int nbatch, hipSt
       use_big(g.M, g.N, t256))
     return launch_persist<T, TO>(akout, bkout, shift, g, (int)t256, buf, st);
   if (dma && g.force_regstage != 2 && use_big(g.M, g.N, t256)) {
-    if constexpr (sizeof(T) == 2)
-      if (tt::opt(tt::OPT_GEMM_A3) && buf)
-        return launch_t<T, TO, 256, 256, 2, 4, true, true, true>(akout, bkout, shift, g, t256, st);
+    if (tt::opt(tt::OPT_GEMM_A3) && buf)
+      return launch_t<T, TO, 256, 256, 2, 4, true, true, true>(akout, bkout, shift, g, t256, st);
     if (tt::opt(tt::OPT_GEMM_A3)) return launch_t<T, TO, 256, 256, 2, 4, true, true>(akout, bkout, shift, g, t256, st);
     return launch_t<T, TO, 256, 256, 2, 4, true>(akout, bkout, shift, g, t256, st);
   }

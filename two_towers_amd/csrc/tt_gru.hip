@@ -358,6 +358,9 @@ TT_DEV void unpack8(uint4 v, float (&f)[8]) {
 #ifndef TT_BWD_BUF  // backward product DMAs through buffer resources (0: per-lane pointers)
 #define TT_BWD_BUF 1
 #endif
+#ifndef TT_BWD_NB  // gru_bwd_rows: epilogue rows whose loads are in flight together
+#define TT_BWD_NB 2
+#endif
 #ifndef TT_BWD_NT
 #define TT_BWD_NT 3
 #endif
@@ -801,7 +804,7 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int e = 0; e < 8; ++e) bsum[q][e] = 0.f;
-    constexpr int NB = 2;
+    constexpr int NB = TT_BWD_NB;  // rows per batch of epilogue loads
     auto batch = [&](const int kb) {
       uint4 vin[NB][7];
 #pragma unroll
@@ -1256,6 +1259,9 @@ __global__ __launch_bounds__(PNT) void gru_fwd_seq(FwdArgs a) {
 // gru_fwd_seq). Every wait is bounded: a wait that gives up marks the launch (per-launch flag,
 // so the rest of the launch drains quickly) and sets the caller's status word (sticky).
 typedef __attribute__((address_space(1))) unsigned xc_gu32;
+#ifndef XC_G_AUX  // cache policy of the column-split forward's G loads (2: non-temporal)
+#define XC_G_AUX 0
+#endif
 #ifndef XC_OUT_AUX
 #define XC_OUT_AUX 0
 #endif
@@ -1490,7 +1496,7 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
     const uint32_t og = c * xc::CR + cr < q.nrow ? (uint32_t)(((c * xc::CR + cr) * T_ + q.t) * (int)a.ldg + j) * 2u
                                                   : xc::OOB;
 #pragma unroll
-    for (int g = 0; g < 3; ++g) gx[g] = __builtin_amdgcn_raw_buffer_load_b128(rG, (int)og, g * H * 2, 0);
+    for (int g = 0; g < 3; ++g) gx[g] = __builtin_amdgcn_raw_buffer_load_b128(rG, (int)og, g * H * 2, XC_G_AUX);
   };
   // h chunk c of step q (from the image of step idx - 1), or zeros at a round's first step
   tt_u32x4 hv[C::QPW];

@@ -85,3 +85,26 @@ def test_buffer_dma_split_k_wgrad_hh_composition():
             hs[:, :-1] = h[:, 1:]
         ref = dgh.t() @ hs.reshape(K, H)
         assert _rel(c1[d], ref) < 1e-5, (d, _rel(c1[d], ref))
+
+
+def test_persistent_tile_order_is_bit_identical():
+    """gemm_persist's column-group-per-XCD tile walk (option gemm_order 1) computes every
+    tile exactly as the row-panel walk (0) does: the input-projection shape class, two batch
+    entries, 12 column panels (3 groups of 4), 64 row panels."""
+    m, n, k = 16384, 3072, 1024
+    g = torch.Generator().manual_seed(51)
+    A = [torch.randn(m, k, generator=g).to(torch.bfloat16).to(DEV) for _ in range(2)]
+    B = [torch.randn(n, k, generator=g).to(torch.bfloat16).to(DEV) for _ in range(2)]
+    bias = [torch.randn(n, generator=g).to(DEV) for _ in range(2)]
+    outs = []
+    for order in (0, 1):
+        C = [torch.empty(m, n, device=DEV, dtype=torch.bfloat16) for _ in range(2)]
+        with option("gemm_order", order):
+            ops.gemm(A, B, C, m=m, n=n, k=k, lda=k, ldb=k, ldc=n, a_kouter=False, b_kouter=False,
+                     dtype=torch.bfloat16, out_dtype=torch.bfloat16, bias=bias, splits=1)
+        outs.append(C)
+    torch.cuda.synchronize()
+    for i in range(2):
+        assert torch.equal(outs[0][i], outs[1][i]), i
+        ref = A[i].float() @ B[i].float().t() + bias[i]
+        assert _rel(outs[1][i].float(), ref) < 1e-2

@@ -39,6 +39,7 @@ constexpr OptDef kOpts[OPT_N] = {
     {"gru_xc_spins", "TT_GRU_XC_SPINS", 22},      {"gru_bwd_skew", "TT_GRU_BWD_SKEW", 14},
     {"gru_fwd_skew", "TT_GRU_FWD_SKEW", 0},       {"gemm_bres", "TT_GEMM_BRES", 1},
     {"gru_xc_coop", "TT_GRU_XC_COOP", 1},         {"gemm_buf", "TT_GEMM_BUF", 1},
+    {"gemm_order", "TT_GEMM_ORDER", 1},
 };
 struct OptTable {
   std::atomic<int> v[OPT_N];
@@ -100,6 +101,8 @@ struct GemmArgs {
   int skew;  // persistent GEMM start skew (OPT_GEMM_SKEW)
   int bias_vec_ok;  // every bias pointer 16-byte aligned
   int stream_out;   // write-through (sc1) output stores: big outputs
+  int walk_g, walk_x;  // gemm_persist tile walk: column panels per group, workgroup sets (0: default)
+  int nbatch;
 };
 
 constexpr int BM = 128, BN = 128;  // tile of the register-staged / small path
@@ -525,6 +528,22 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
   const int nwg = gridDim.x;
   const int w = xcd_remap(blockIdx.x, nwg);
   if (w >= ntiles) return;
+  // Tile walk. Default: tile q = w, w + nwg, ... (n-tile fastest), so at any time an XCD's
+  // 32 workgroups cover ~3 row panels x ALL column panels: every B panel is re-fetched from
+  // the Infinity Cache once per row panel when B exceeds the XCD's L2 (input_proj_l1: W_ih
+  // 6 MiB per tower). g.order (option gemm_order, when nwg = 256, 256 | ntiles and 4 | ntn):
+  // tiles are grouped in units of 4 column panels x 1 row panel, units ordered column group
+  // first, and XCD x walks its own contiguous eighth of them 32 at a time -- 8 row panels x
+  // the same 4 column panels per round, so 4 B panels (2 MiB at K 1024) stay in its L2.
+  // Both walks are one formula (host-set g.walk_g / g.walk_x; 0 = the default walk): tile
+  // q = ((group * nbatch + bi) * ntm + mt) * G + j covers column panel group * G + j, and the
+  // workgroups are split into X equal sets that walk consecutive spans of q.
+  const int G = g.walk_g > 0 ? g.walk_g : (g.N + 255) / 256;
+  const int X = g.walk_x > 0 ? g.walk_x : 1;
+  const int P = nwg / X, span = ntiles / X;
+  const int qbeg = (w / P) * span + w % P;
+  const int qstep = P;
+  const int qend = (w / P + 1) * span;
   // optional start skew: workgroups in four phases, so the tiles' output bursts (all CUs
   // finish a tile at about the same time otherwise) spread over the tile period
   for (int i = 0; i < (w & 3) * g.skew; ++i) __builtin_amdgcn_s_sleep(64);
@@ -538,36 +557,37 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
   struct TileId { int bi, m0, n0; };
   auto decode = [&](int q) {
     TileId t;
-    t.bi = q / (ntm * ntn);
-    const int tile = q - t.bi * (ntm * ntn);
-    t.m0 = (tile / ntn) * 256;
-    t.n0 = (tile % ntn) * 256;
+    const int u = q / G, per = g.nbatch * ntm;
+    const int gr = u / per, rr = u - gr * per;
+    t.bi = rr / ntm;
+    t.m0 = (rr - t.bi * ntm) * 256;
+    t.n0 = (gr * G + (q - u * G)) * 256;
     return t;
   };
   // A / B loaders of tile q (q >= ntiles: a loader whose pieces are all out of range)
   auto loader_a = [&](int q) {
-    const TileId t = decode(q < ntiles ? q : 0);
+    const TileId t = decode(q < qend ? q : 0);
     const T* A = static_cast<const T*>(g.a[t.bi]);
     if constexpr (AKO) {
-      ttg::KOPlain<T> la{A, g.lda, t.m0, q < ntiles ? g.M - t.m0 : 0};
+      ttg::KOPlain<T> la{A, g.lda, t.m0, q < qend ? g.M - t.m0 : 0};
       if (g.a_split > 0) {
         la.base1 = static_cast<const T*>(g.a_hi[t.bi]);
         la.csplit = g.a_split;
       }
       return la;
     } else {
-      return ttg::KCPlain<T>{A, g.lda, t.m0, q < ntiles ? g.M : t.m0};
+      return ttg::KCPlain<T>{A, g.lda, t.m0, q < qend ? g.M : t.m0};
     }
   };
   auto loader_b = [&](int q) {
-    const TileId t = decode(q < ntiles ? q : 0);
+    const TileId t = decode(q < qend ? q : 0);
     const T* B = static_cast<const T*>(g.b[t.bi]);
     if constexpr (!BKO) {
-      return ttg::KCPlain<T>{B, g.ldb, t.n0, q < ntiles ? g.N : t.n0};
+      return ttg::KCPlain<T>{B, g.ldb, t.n0, q < qend ? g.N : t.n0};
     } else if constexpr (SHIFT) {
-      return ttg::KOShift<T>{B, g.ldb, t.n0, q < ntiles ? g.N - t.n0 : 0, g.seq_t, g.bshift[t.bi]};
+      return ttg::KOShift<T>{B, g.ldb, t.n0, q < qend ? g.N - t.n0 : 0, g.seq_t, g.bshift[t.bi]};
     } else {
-      return ttg::KOPlain<T>{B, g.ldb, t.n0, q < ntiles ? g.N - t.n0 : 0};
+      return ttg::KOPlain<T>{B, g.ldb, t.n0, q < qend ? g.N - t.n0 : 0};
     }
   };
 #ifdef TT_DIAG
@@ -578,7 +598,7 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{(float)i, (float)j, 1.f, 2.f};
-      for (int q = w; q < ntiles; q += nwg) {
+      for (int q = qbeg; q < qend; q += qstep) {
         const TileId t = decode(q);
         const bool full = t.m0 + 256 <= g.M && t.n0 + 256 <= g.N && g.vec_ok;
         epi_direct<TO>(g, acc, static_cast<TO*>(g.c[t.bi]), g.bias[t.bi], t.m0, t.n0, wm, wn, full);
@@ -587,8 +607,8 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
     }
   }
 #endif
-  auto la = loader_a(w);
-  auto lb = loader_b(w);
+  auto la = loader_a(qbeg);
+  auto lb = loader_b(qbeg);
   typename L8::template Half<AKO, decltype(la)> pa0, pa1;
   typename L8::template Half<BKO, decltype(lb)> pb0, pb1;
   pa0.init(la, 0, nk, g.K, 0);
@@ -622,8 +642,8 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
   int as = 0;   // A3: A slot of the stream's current K-tile (git mod 3)
   int ra_off = 0, rb_off = 0;  // K-tile index of the A / B pieces' tile start in this tile's terms
   bool epi_full = false;       // A3: the previous tile's epilogue issued EPI_STORES<TO> stores per wave
-  for (int q = w; q < ntiles; q += nwg) {
-    const int qn = q + nwg;
+  for (int q = qbeg; q < qend; q += qstep) {
+    const int qn = q + qstep;
     const TileId cur_t = decode(q);
     f32x4 acc[8][4];
 #pragma unroll
@@ -800,7 +820,7 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
       }
       __builtin_amdgcn_s_barrier();  // staging free for the next pass
     }
-    if (late && qn < ntiles) __builtin_amdgcn_s_barrier();  // re-stagger for the next tile
+    if (late && qn < qend) __builtin_amdgcn_s_barrier();  // re-stagger for the next tile
   }
   if constexpr (A3)
     if (!late) __builtin_amdgcn_s_barrier();  // the late row's extra prologue barrier
@@ -849,8 +869,17 @@ int launch_t(int akout, int bkout, bool shift, const GemmArgs& g, long nwg, hipS
 inline bool use_big(int m, int n, long tiles256) { return m >= 256 && n >= 256 && tiles256 >= 256; }
 
 template <typename T, typename TO>
-int launch_persist(int akout, int bkout, bool shift, const GemmArgs& g, int ntiles, bool buf, hipStream_t st) {
+int launch_persist(int akout, int bkout, bool shift, const GemmArgs& g0, int ntiles, bool buf, hipStream_t st) {
   dim3 grid((unsigned)std::min(ntiles, 256)), blk(512);
+  // option gemm_order: column groups of 4 panels per XCD (each XCD's 32 workgroups walk
+  // their own eighth of the tiles: 8 row panels x the same 4 column panels per round, so
+  // those B panels stay in the XCD's L2); needs 256 workgroups, 256 | tiles, 4 | column panels
+  GemmArgs g = g0;
+  g.walk_g = g.walk_x = 0;
+  if (tt::opt(tt::OPT_GEMM_ORDER) && ntiles % 256 == 0 && ((g.N + 255) / 256) % 4 == 0) {
+    g.walk_g = 4;
+    g.walk_x = 8;
+  }
 #define TT_L(AK, BK, SH, A3, BUF) \
   hipLaunchKernelGGL((gemm_persist<T, AK, BK, SH, TO, A3, BUF>), grid, blk, 0, st, g, ntiles)
 #define TT_L2(AK, BK, SH) \
@@ -1018,6 +1047,7 @@ extern "C" int tt_gemm(int dtype, int out_dtype, int a_kouter, int b_kouter, int
   g.M = m; g.N = n; g.K = k;
   g.alpha = alpha; g.beta = beta_accum; g.relu = relu; g.seq_t = seq_t;
   g.force_regstage = tt::opt(tt::OPT_GEMM_REGSTAGE);
+  g.nbatch = nbatch;
   g.skew = tt::opt(tt::OPT_GEMM_SKEW);
   g.drop_seed = drop_seed;
   g.drop_row0 = batch->drop_row0;

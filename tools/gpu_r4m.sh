@@ -1,8 +1,8 @@
 # fp32 buffer DMAs and the column-group tile walk (parity), GEMM A/B, backward epilogue batch NB 4, forward G loads non-temporal, configs[1] line
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_gemm_buf.py tests/test_gpu_kernels.py tests/test_gpu_golden.py > gpurun_out/r4m_pytest.txt 2>&1; rc=$?; tail -3 gpurun_out/r4m_pytest.txt
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_gemm_buf.py tests/test_gpu_kernels.py tests/test_gpu_golden.py tests/test_gpu_model.py tests/test_gpu_bench_path.py > gpurun_out/r4m_pytest.txt 2>&1; rc=$?; tail -3 gpurun_out/r4m_pytest.txt
 [ $rc -eq 0 ] || exit $rc
-for rep in 1 2; do for lib in libtt_hip.so libtt_hip_nb4.so; do
+for rep in 1 2; do for lib in libtt_hip.so libtt_hip_s0.so libtt_hip_nb4.so; do
   echo "== $lib"; TT_HIP_LIB=$GRAFT_REPO_ROOT/two_towers_amd/lib/$lib timeout -k 10 200 python tools/bench_gru.py --variants "" --bwd-variants P:0:2:14,P:0:2:0,P:0:2:7 --iters 5 || exit 1
 done; done > gpurun_out/r4m_bwd.txt 2>&1
 grep -v amdgpu gpurun_out/r4m_bwd.txt

@@ -358,6 +358,9 @@ TT_DEV void unpack8(uint4 v, float (&f)[8]) {
 #ifndef TT_BWD_BUF  // backward product DMAs through buffer resources (0: per-lane pointers)
 #define TT_BWD_BUF 1
 #endif
+#ifndef TT_BWD_STAG  // gru_bwd_rows product: wave rows one barrier apart (0: lockstep)
+#define TT_BWD_STAG 1
+#endif
 #ifndef TT_BWD_NB  // gru_bwd_rows: epilogue rows whose loads are in flight together
 #define TT_BWD_NB 2
 #endif
@@ -751,6 +754,50 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
       issue(0);
       issue(1);
       issue(2);
+#if TT_BWD_STAG
+      // The two wave rows run one barrier apart (wave row 1 late), two barriers per K-tile:
+      // each wave reads ALL of K-tile r's fragments after the K-tile's start barrier and
+      // retires them before its mid barrier, so one row's reads and DMA issue overlap the
+      // other row's MFMAs. Slot (r + 3) % 4 = r - 1's is refilled after K-tile r's start
+      // barrier: both rows retired their reads of r - 1 by then. Tile r + 1 must be waited
+      // for (every wave, its own pieces) before absolute barrier 2r + 2: the early row's
+      // next start barrier, the late row's mid barrier of r.
+      const bool late = wr == 1;
+      wait_younger<C::NS - 2, C::P>(NK - 1);  // tile 0 landed
+      __builtin_amdgcn_s_barrier();
+      if (late) __builtin_amdgcn_s_barrier();
+#pragma unroll 1
+      for (int r = 0; r < NK; ++r) {
+        if (r > 0) __builtin_amdgcn_s_barrier();  // start of K-tile r
+        if (r + 3 < NK) issue(r + 3);
+        const char* sl = lds + (r % C::NS) * C::SLOT;
+        uint4 fa[4], fb[C::NCB];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = frag_kc64(sl, wr * 64 + 16 * i);
+        const char* ib = sl + 8192 + ((wc * (C::HP / 4)) >> 7) * 8192;
+        const int cb = (wc * (C::HP / 4)) & 127;
+#pragma unroll
+        for (int j = 0; j < C::NCB; ++j) fb[j] = ttg::frag<bf16_t, true>(ib, cb + 16 * j, 0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int j = 0; j < C::NCB / 2; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i][j] = ttg::mma<bf16_t>(fb[j], fa[i], acc[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of tile r retired
+        __builtin_amdgcn_sched_barrier(0);
+        if (late) wait_younger<C::NS - 2, C::P>(NK - 2 - r);  // tile r + 1 landed
+        __builtin_amdgcn_s_barrier();                          // mid
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int j = C::NCB / 2; j < C::NCB; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i][j] = ttg::mma<bf16_t>(fb[j], fa[i], acc[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+        if (!late) wait_younger<C::NS - 2, C::P>(NK - 2 - r);  // tile r + 1 landed
+      }
+      if (!late) __builtin_amdgcn_s_barrier();  // the late row's extra barrier
+#else
 #pragma unroll 1
       for (int r = 0; r < NK; ++r) {
         wait_younger<C::NS - 2, C::P>(NK - 1 - r);  // tile r landed (up to 2 younger in flight)
@@ -776,6 +823,7 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
           __builtin_amdgcn_s_setprio(0);
         }
       }
+#endif
       __builtin_amdgcn_s_barrier();  // every wave done with the slots before the staging
     }
     // ---- epilogue: as gru_bwd_rows

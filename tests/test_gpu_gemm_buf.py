@@ -55,12 +55,14 @@ def test_buffer_dma_gemm_is_bit_identical(akout, bkout, path, dt):
     assert _rel(c1.double(), ref) < (1e-2 if dt == torch.bfloat16 else 1e-5)
 
 
-def test_buffer_dma_split_k_wgrad_hh_composition():
+@pytest.mark.parametrize("T", [32, 64, 128])
+def test_buffer_dma_split_k_wgrad_hh_composition(T):
     """dW_hh's GEMM: A = dL/dgh^T through the split-column loader (r|z columns of dG, the
-    W_hn block at column 6H), B = h_{t-1} (time-shifted, pointer DMAs), split-K."""
-    H, Bsz, T = 256, 512, 32
-    K = Bsz * T
-    g = torch.Generator().manual_seed(41)
+    W_hn block at column 6H), B = h_{t-1} (time-shifted: the masked k-rows are the same lanes
+    of every K-tile at T 32 / 64, one k-row of every other K-tile at T 128), split-K."""
+    H, K = 256, 16384
+    Bsz = K // T
+    g = torch.Generator().manual_seed(41 + T)
     dG = torch.randn(K, 8 * H, generator=g).to(torch.bfloat16).to(DEV)
     Y = torch.randn(K, 2 * H, generator=g).to(torch.bfloat16).to(DEV)
     a = [dG[:, d * 3 * H:] for d in range(2)]

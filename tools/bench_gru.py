@@ -12,8 +12,11 @@ from two_towers_amd import _lib  # noqa: E402
 from two_towers_amd._lib import GruBwdRec, GruFwdRec, call, set_option, stream_ptr  # noqa: E402
 
 
+DT = torch.bfloat16
+
+
 def setup(B, T, H, dev):
-    dt = torch.bfloat16
+    dt = DT
     n = 2
     G = [torch.randn(B * T, 6 * H, device=dev).to(dt) for _ in range(n)]
     whh = [[(torch.randn(3 * H, H, device=dev) * H ** -0.5).to(dt) for _ in range(2)] for _ in range(n)]
@@ -41,7 +44,7 @@ def setup(B, T, H, dev):
 
 
 def setup_bwd(B, T, H, keep, dev):
-    dt = torch.bfloat16
+    dt = DT
     G, whh, bhn, Y, X1, S, hs = keep
     n = 2
     dY = [torch.randn(B * T, 2 * H, device=dev).to(dt) * 0.01 for _ in range(n)]
@@ -68,7 +71,7 @@ def setup_bwd(B, T, H, keep, dev):
 
 
 def fwd_call(recs, a, st, ws):
-    call("tt_gru_fwd", 1, recs, 4, a.B, a.T, a.H, 6 * a.H, 2 * a.H, 0.1,
+    call("tt_gru_fwd", 0 if DT == torch.float32 else 1, recs, 4, a.B, a.T, a.H, 6 * a.H, 2 * a.H, 0.1,
          ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0, st)
 
 
@@ -83,12 +86,15 @@ def main():
                          "xcx (members dealt over XCDs), seq (row-owning), step (per-step)")
     ap.add_argument("--bwd-variants", default="P:0:2", help="rows:dbg:streams[:skew]; rows P (row-owning), S (128x128 "
                     "per-step, `streams` chains), 128 / 64 (per-step 256x256 / 128-row tiles); skew: option gru_bwd_skew")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     a = ap.parse_args()
+    global DT
+    DT = torch.float32 if a.dtype == "fp32" else torch.bfloat16
     dev = torch.device("cuda")
     recs, keep = setup(a.B, a.T, a.H, dev)
     st = stream_ptr(dev)
     set_option("gru_fwd_xc", 2)
-    nb = _lib.load().tt_gru_fwd_ws_size(1, 4, a.B, a.T, a.H, 6 * a.H, 2 * a.H)
+    nb = _lib.load().tt_gru_fwd_ws_size(0 if DT == torch.float32 else 1, 4, a.B, a.T, a.H, 6 * a.H, 2 * a.H)
     ws = torch.zeros(max(nb, 256), dtype=torch.uint8, device=dev) if nb else None
     fwd_call(recs, a, st, ws)  # real S / Y for the backward
     for v in a.bwd_variants.split(","):
@@ -103,7 +109,7 @@ def main():
         os.environ["TT_GRU_DBG"] = dbg  # read only by a -DTT_DIAG build
         set_option("gru_bwd_streams", int(strm))
         brecs, bkeep = setup_bwd(a.B, a.T, a.H, keep, dev)
-        f = lambda: call("tt_gru_bwd", 1, brecs, 4, a.B, a.T, a.H, 2 * a.H, 8 * a.H, 2 * a.H, st)
+        f = lambda: call("tt_gru_bwd", 0 if DT == torch.float32 else 1, brecs, 4, a.B, a.T, a.H, 2 * a.H, 8 * a.H, 2 * a.H, st)
         f()
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -39,7 +39,7 @@ constexpr OptDef kOpts[OPT_N] = {
     {"gru_xc_spins", "TT_GRU_XC_SPINS", 22},      {"gru_bwd_skew", "TT_GRU_BWD_SKEW", 14},
     {"gru_fwd_skew", "TT_GRU_FWD_SKEW", 0},       {"gemm_bres", "TT_GEMM_BRES", 1},
     {"gru_xc_coop", "TT_GRU_XC_COOP", 1},         {"gemm_buf", "TT_GEMM_BUF", 1},
-    {"gemm_order", "TT_GEMM_ORDER", 1},
+    {"gemm_order", "TT_GEMM_ORDER", 0},
 };
 struct OptTable {
   std::atomic<int> v[OPT_N];
@@ -956,10 +956,7 @@ int launch_gemm(int akout, int bkout, bool shift, GemmArgs& g, int nbatch, hipSt
   {
     const long span = (long)(g.kt_per_split + 2) * (ttg::KTB / (int)sizeof(T)) * (long)sizeof(T);
     if (akout && span * g.lda >= (1L << 32)) buf = false;
-    if (bkout && span * g.ldb >= (1L << 32)) buf = false;
-    // the time-shifted B operand: sequence boundaries whole-K-tile aligned or within one K-tile
-    const int kte = ttg::KTB / (int)sizeof(T);
-    if (shift && !(g.seq_t > 0 && (kte % g.seq_t == 0 || g.seq_t % kte == 0))) buf = false;
+    if (bkout && !shift && span * g.ldb >= (1L << 32)) buf = false;
     if (!akout && (long)256 * g.lda * (long)sizeof(T) >= (1L << 31)) buf = false;
     if (!bkout && (long)256 * g.ldb * (long)sizeof(T) >= (1L << 31)) buf = false;
     for (int b = 0; b < 4 && g.a_split > 0; ++b) {

@@ -573,13 +573,6 @@ struct Loop8 {
     tt_rsrc4 rs;
     uint32_t delta;
     uint32_t voff[2];
-    // SHIFTED (the time-shifted h_{t-1} operand): K-rows whose source time t + shift falls
-    // outside [0, T) must read zero. When T divides KTE those are the same lanes in every
-    // K-tile (folded into voff); when KTE divides T they are one k-row of the K-tiles that
-    // start (shift -1) or end (shift +1) a sequence: vb holds the masked offsets, chosen
-    // per K-tile by a wave-uniform test (sel: 0 none, 1 start, 2 end)
-    uint32_t vb[2];
-    int sel, kt0, T_;
   };
   template <bool KO, class L>
   TT_DEV static void init_buf(const L& ld, int kt0, int K, int roff, BufHalf& h) {
@@ -600,17 +593,10 @@ struct Loop8 {
       }
     } else {
       const long k0 = (long)kt0 * KTE;
-      int shift = 0;
-      if constexpr (L::SHIFTED) shift = ld.shift;
       long nrec = K > k0 ? ((long)K - k0) * ld.ld * (long)sizeof(T) : 0;
       nrec = nrec > 0xFFFFFFFFL ? 0xFFFFFFFFL : nrec;
-      // SHIFTED: based at source row k0 + shift (a row before the buffer when k0 = 0 and
-      // shift = -1: that row is always masked)
-      h.rs = make_rsrc4(ld.base + (k0 + shift) * ld.ld, (uint32_t)nrec);
+      h.rs = make_rsrc4(ld.base + k0 * ld.ld, (uint32_t)nrec);
       h.delta = (uint32_t)((long)KTE * ld.ld * (long)sizeof(T));
-      h.sel = 0;
-      h.kt0 = kt0;
-      h.T_ = 1;
       constexpr int CPR = 128 * (int)sizeof(T) / 16;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -619,34 +605,15 @@ struct Loop8 {
         int c;
         if constexpr (sizeof(T) == 2) c = q ^ (ko_v(kl) << 1);
         else c = q ^ (((kl >> 2) & 1) << 2);
-        int co;
-        if constexpr (L::SHIFTED) co = ld.c0 + roff + c * EPC;
-        else co = (int)ld.col_off(roff + c * EPC);
-        h.voff[j] = (uint32_t)(((long)kl * ld.ld + co) * (long)sizeof(T));
-        h.vb[j] = h.voff[j];
-        if constexpr (L::SHIFTED) {
-          const int T_ = ld.T_;
-          const int edge = shift < 0 ? 0 : T_ - 1;  // the time step with no source row
-          if (KTE % T_ == 0) {  // the same lanes of every K-tile
-            if (kl % T_ == edge) h.voff[j] = 0x80000000u;
-          } else {              // T_ % KTE == 0 (host-checked): one k-row of some K-tiles
-            h.T_ = T_;
-            h.sel = shift < 0 ? 1 : 2;
-            if (kl == (shift < 0 ? 0 : KTE - 1)) h.vb[j] = 0x80000000u;
-          }
-        }
+        h.voff[j] = (uint32_t)(((long)kl * ld.ld + ld.col_off(roff + c * EPC)) * (long)sizeof(T));
       }
     }
   }
   TT_DEV static void issue_buf(const BufHalf& h, int r, uint32_t img) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)r * h.delta);
-    // sel 1: this K-tile starts a sequence; sel 2: it ends one (wave-uniform)
-    const int kt = h.kt0 + r;
-    const bool m = h.sel == 1 ? (kt * KTE) % h.T_ == 0 : h.sel == 2 ? ((kt + 1) * KTE) % h.T_ == 0 : false;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-      dma16_buf(h.rs, m ? h.vb[j] : h.voff[j], soff, img + (uint32_t)(wave + 8 * j) * 1024u);
+    for (int j = 0; j < 2; ++j) dma16_buf(h.rs, h.voff[j], soff, img + (uint32_t)(wave + 8 * j) * 1024u);
   }
   // One half-tile source: Piece form (any loader) or buffer form (BUF, plain loaders).
   template <bool KO, class L>
@@ -668,7 +635,7 @@ struct Loop8 {
     TT_DEV void issue(int r, uint32_t img) const { issue_buf(h, r, img); }
   };
   template <bool KO, class L>
-  using Half = std::conditional_t<BUF && !L::KSPLIT, BHalf<KO, L>, PHalf<KO, L>>;
+  using Half = std::conditional_t<BUF && !L::SHIFTED && !L::KSPLIT, BHalf<KO, L>, PHalf<KO, L>>;
 
   TT_DEV static void quad(int mi, int ni, const uint4 (&fa)[2][4], const uint4 (&fb)[2][4], f32x4 (&acc)[TM][TN]) {
     __builtin_amdgcn_s_barrier();

@@ -39,7 +39,8 @@ enum Opt {
   OPT_GEMM_BRES,        // 0: no B-resident short-K GEMM (layer-0 input projection)
   OPT_GRU_XC_COOP,      // 0: column-split forward by a plain launch (occupancy-checked) instead of a cooperative one
   OPT_GEMM_BUF,         // 0: 256x256 GEMM operand DMAs through per-lane pointers instead of buffer resources
-  OPT_GEMM_ORDER,       // 0: persistent GEMM tiles in row-panel order instead of column groups per XCD
+  OPT_GEMM_ORDER,       // 1: persistent GEMM tiles in column groups per XCD
+  OPT_GRU_STEP_RING,    // LDS stages of the per-step GRU kernels' product (2: double buffer; fwd uses <= 3)
   OPT_N
 };
 int opt(Opt o);

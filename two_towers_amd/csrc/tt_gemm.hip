@@ -39,7 +39,7 @@ constexpr OptDef kOpts[OPT_N] = {
     {"gru_xc_spins", "TT_GRU_XC_SPINS", 22},      {"gru_bwd_skew", "TT_GRU_BWD_SKEW", 14},
     {"gru_fwd_skew", "TT_GRU_FWD_SKEW", 0},       {"gemm_bres", "TT_GEMM_BRES", 1},
     {"gru_xc_coop", "TT_GRU_XC_COOP", 1},         {"gemm_buf", "TT_GEMM_BUF", 1},
-    {"gemm_order", "TT_GEMM_ORDER", 0},
+    {"gemm_order", "TT_GEMM_ORDER", 0},           {"gru_step_ring", "TT_GRU_STEP_RING", 4},
 };
 struct OptTable {
   std::atomic<int> v[OPT_N];

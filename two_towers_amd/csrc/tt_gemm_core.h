@@ -408,14 +408,22 @@ TT_DEV uint4 frag2(const char* img, int r0, int ks) {
   else return frag<T, true>(img + (r0 >> 7) * Img2<T, true, 128>::KOSUB, r0 & 127, ks);
 }
 
-template <typename T, bool AKO, bool BKO, int BM, int BN, int WGM, int WGN>
+// NS LDS stages: NS = 2 waits for each K-tile's DMAs with vmcnt(0) right before it is read
+// (one K-tile in flight during the MFMAs); NS > 2 keeps NS - 1 K-tiles in flight with a
+// counted wait (the DMAs of the younger K-tiles), for loops whose K-tile of MFMAs is short
+// against the operand's load latency (the fp32 per-step GRU kernels at small batch).
+template <typename T, bool AKO, bool BKO, int BM, int BN, int WGM, int WGN, int NS = 2>
 struct DLoop {
   static constexpr int NW = WGM * WGN;
   static constexpr int NT = 64 * NW;
   using IA = Img2<T, AKO, BM>;
   using IB = Img2<T, BKO, BN>;
   static constexpr int STAGE = IA::BYTES + IB::BYTES;
-  static constexpr int LDS_BYTES = 2 * STAGE;
+  static constexpr int LDS_BYTES = NS * STAGE;
+  // this wave's DMAs per K-tile (the fewest over the waves: a wave that issues more waits
+  // for some of its younger DMAs too, which is safe)
+  static constexpr int DPW = (IA::CHUNKS / 64) / NW + (IB::CHUNKS / 64) / NW;
+  static_assert(NS >= 2 && NS <= 4 && (NS - 2) * DPW <= 63, "DLoop stages");
   static constexpr int WTM = BM / WGM, WTN = BN / WGN;  // wave tile
   static constexpr int TM = WTM / 16, TN = WTN / 16;
   static_assert(IA::CHUNKS % 64 == 0 && IB::CHUNKS % 64 == 0, "tile/wave mismatch");
@@ -425,9 +433,52 @@ struct DLoop {
 
   // Accumulates K-tiles [kt0, kt1) into acc (caller zeroes it); ends with a barrier.
   template <class LA, class LB>
+  TT_DEV static void mma_tile(const char* ia, int wm, int wn, f32x4 (&acc)[TM][TN]) {
+    const char* ib = ia + IA::BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = frag2<T, AKO>(ia, wm + 16 * i, ks);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = frag2<T, BKO>(ib, wn + 16 * j, ks);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mma<T>(fa[i], fb[j], acc[i][j]);
+    }
+  }
+  template <class LA, class LB>
   TT_DEV static void run(const LA& la, const LB& lb, int K, int kt0, int kt1, char* lds, f32x4 (&acc)[TM][TN]) {
     if (kt0 >= kt1) return;
     const int wm = wave_m0(), wn = wave_n0();
+    if constexpr (NS > 2) {
+#pragma unroll
+      for (int i = 0; i < NS - 1; ++i)
+        if (kt0 + i < kt1) {
+          stage_dma2<T, AKO, BM, NW>(la, kt0 + i, K, lds + i * STAGE);
+          stage_dma2<T, BKO, BN, NW>(lb, kt0 + i, K, lds + i * STAGE + IA::BYTES);
+        }
+      int rd = 0, wr = NS - 1;  // slots of K-tile kt and of K-tile kt + NS - 1
+      for (int kt = kt0; kt < kt1; ++kt) {
+        // K-tiles younger than kt already issued: min(NS - 2, kt1 - 1 - kt)
+        const int younger = kt1 - 1 - kt;
+        if (younger >= NS - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * DPW) : "memory");
+        else if (NS == 4 && younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave's DMAs of kt landed; slot wr was read at kt - 1
+        if (kt + NS - 1 < kt1) {
+          char* nx = lds + wr * STAGE;
+          stage_dma2<T, AKO, BM, NW>(la, kt + NS - 1, K, nx);
+          stage_dma2<T, BKO, BN, NW>(lb, kt + NS - 1, K, nx + IA::BYTES);
+        }
+        mma_tile<LA, LB>(lds + rd * STAGE, wm, wn, acc);
+        rd = rd == NS - 1 ? 0 : rd + 1;
+        wr = wr == NS - 1 ? 0 : wr + 1;
+      }
+      __builtin_amdgcn_s_barrier();
+      return;
+    }
     stage_dma2<T, AKO, BM, NW>(la, kt0, K, lds);
     stage_dma2<T, BKO, BN, NW>(lb, kt0, K, lds + IA::BYTES);
     for (int kt = kt0; kt < kt1; ++kt) {

@@ -88,10 +88,10 @@ struct GateRows {
 // half the W_hh traffic per FLOP and twice the MFMA work per K-tile barrier): at configs[4]
 // (H 1024, B 8192) 48.0-48.6 vs 50.3-51.5 ms per layer. A 4-stage LDS ring with counted
 // waits on 128-row tiles (one workgroup per CU) measured 85.7 ms.
-template <typename T, int BMR>
+template <typename T, int BMR, int NS = 2>  // NS: LDS stages of the product (DLoop)
 __global__ __launch_bounds__(2 * BMR) void gru_fwd_step(FwdArgs a) {
   constexpr int NT = 2 * BMR;
-  using ML = ttg::DLoop<T, false, false, BMR, 192, BMR / 64, 2>;
+  using ML = ttg::DLoop<T, false, false, BMR, 192, BMR / 64, 2, NS>;
   __shared__ __attribute__((aligned(16))) char lds[ML::LDS_BYTES];
   // 1-D grid, XCD-aware: the H/64 unit tiles of one batch tile are consecutive ids on one
   // XCD, so its h_{s-1} panel is fetched into that XCD's L2 once, not once per tile.
@@ -192,9 +192,10 @@ __global__ __launch_bounds__(2 * BMR) void gru_fwd_step(FwdArgs a) {
   }
 }
 
-template <typename T, int BMR>  // BMR batch rows per tile: 128, or 64 (3 tiles per CU)
+// BMR batch rows per tile: 128, or 64 (3 tiles per CU at NS 2); NS: LDS stages (DLoop)
+template <typename T, int BMR, int NS = 2>
 __global__ __launch_bounds__(256) void gru_bwd_step(BwdArgs a) {
-  using ML = ttg::DLoop<T, false, true, BMR, 128, 2, 2>;
+  using ML = ttg::DLoop<T, false, true, BMR, 128, 2, 2, NS>;
   constexpr int LDSB = ML::LDS_BYTES > 64 * 132 * 4 ? ML::LDS_BYTES : 64 * 132 * 4;
   __shared__ __attribute__((aligned(16))) char lds[LDSB];
   const int ntj = (a.H + 127) / 128, ntm = (a.B + BMR - 1) / BMR;
@@ -1999,18 +2000,30 @@ extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B
   if (bmr == 256 && 256L * span >= (1L << 31)) bmr = 128;
   TT_CHECK_ARG((long)bmr * span < (1L << 31), "tt_gru_fwd: tile byte offsets exceed 2 GiB (B tile %d)", bmr);
   dim3 grid(tt_ceil_div(H, 64) * tt_ceil_div(B, bmr) * nrec);
+  // 128-row tiles: a 3-stage product ring when option gru_step_ring >= 3 (120 KiB of LDS)
+  const bool ring = tt::opt(tt::OPT_GRU_STEP_RING) >= 3;
   for (int s = 0; s < T; ++s) {
     a.s = s;
     if (dtype == TT_DT_BF16) {
       if (bmr == 256) hipLaunchKernelGGL((gru_fwd_step<bf16_t, 256>), grid, dim3(512), 0, st, a);
+      else if (ring) hipLaunchKernelGGL((gru_fwd_step<bf16_t, 128, 3>), grid, dim3(256), 0, st, a);
       else hipLaunchKernelGGL((gru_fwd_step<bf16_t, 128>), grid, dim3(256), 0, st, a);
     } else {
       if (bmr == 256) hipLaunchKernelGGL((gru_fwd_step<float, 256>), grid, dim3(512), 0, st, a);
+      else if (ring) hipLaunchKernelGGL((gru_fwd_step<float, 128, 3>), grid, dim3(256), 0, st, a);
       else hipLaunchKernelGGL((gru_fwd_step<float, 128>), grid, dim3(256), 0, st, a);
     }
     TT_CHECK_LAUNCH("gru_fwd_step");
   }
   return 0;
+}
+
+// option gru_step_ring: LDS stages of the per-step backward's product (2: double buffer)
+template <typename T, int BMR>
+static void launch_bwd_step(int ring, dim3 grid, hipStream_t st, const BwdArgs& a) {
+  if (ring >= 4) hipLaunchKernelGGL((gru_bwd_step<T, BMR, 4>), grid, dim3(256), 0, st, a);
+  else if (ring == 3) hipLaunchKernelGGL((gru_bwd_step<T, BMR, 3>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((gru_bwd_step<T, BMR>), grid, dim3(256), 0, st, a);
 }
 
 extern "C" int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B, int T, int H, long ldy,
@@ -2077,16 +2090,17 @@ extern "C" int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B
     TT_CHECK_HIP(hipEventRecord(side->fork, st));
     TT_CHECK_HIP(hipStreamWaitEvent(side->s, side->fork, 0));
   }
+  const int ring = tt::opt(tt::OPT_GRU_STEP_RING);
   for (int s = T - 1; s >= 0; --s) {
     for (int g = 0; g < ngrp; ++g) {
       ga[g].s = s;
       const dim3 grid(tt_ceil_div(H, 128) * tt_ceil_div(B, bmr) * gn[g]);
       if (dtype == TT_DT_BF16) {
-        if (bmr == 64) hipLaunchKernelGGL((gru_bwd_step<bf16_t, 64>), grid, dim3(256), 0, gs[g], ga[g]);
-        else hipLaunchKernelGGL((gru_bwd_step<bf16_t, 128>), grid, dim3(256), 0, gs[g], ga[g]);
+        if (bmr == 64) launch_bwd_step<bf16_t, 64>(ring, grid, gs[g], ga[g]);
+        else launch_bwd_step<bf16_t, 128>(ring, grid, gs[g], ga[g]);
       } else {
-        if (bmr == 64) hipLaunchKernelGGL((gru_bwd_step<float, 64>), grid, dim3(256), 0, gs[g], ga[g]);
-        else hipLaunchKernelGGL((gru_bwd_step<float, 128>), grid, dim3(256), 0, gs[g], ga[g]);
+        if (bmr == 64) launch_bwd_step<float, 64>(ring, grid, gs[g], ga[g]);
+        else launch_bwd_step<float, 128>(ring, grid, gs[g], ga[g]);
       }
       TT_CHECK_LAUNCH("gru_bwd_step");
     }

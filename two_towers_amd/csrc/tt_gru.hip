@@ -110,25 +110,36 @@ __global__ __launch_bounds__(2 * BMR) void gru_fwd_step(FwdArgs a) {
   for (int i = 0; i < ML::TM; ++i)
 #pragma unroll
     for (int j = 0; j < ML::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (s > 0) {
+  bool prod = s > 0, epi = true;
+#ifdef TT_DIAG
+  // diagnostic build, per-step forward (gru_fwd_step): 8 no product, 16 no epilogue
+  if (a.dbg & 8) prod = false;
+  if (a.dbg & 16) epi = false;
+#endif
+  const int tid = threadIdx.x;
+  const int cur = s & 1, prv = cur ^ 1;
+  const T* G = static_cast<const T*>(R.g);
+  const float* hs_prv = R.hs + (long)prv * a.B * H;
+  if (prod) {
     ttg::KCPlain<T> la{Y + (long)tp * a.ldy, (long)T_ * a.ldy, m0, a.B};
     GateRows<T> lb{static_cast<const T*>(R.whh), H, j0};
     const int nk = (H * (int)sizeof(T) + ttg::KTB - 1) / ttg::KTB;
     ML::run(la, lb, H, 0, nk, lds, acc);
   }
+  if (!epi) {
+    if (acc[0][0][0] == 1.2345f) static_cast<T*>(R.y)[0] = T(0);  // keep the product
+    return;
+  }
 
   // ---- epilogue, one 64-row half at a time: stage the fp32 gate tile in LDS, then
   // every thread updates 8 consecutive hidden units of a row with 16-byte accesses.
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, tid = threadIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float* L = reinterpret_cast<float*>(lds);  // [3][64][FLD]
   constexpr int FLD = 68;                    // 64 units + 16 B pad
-  const int cur = s & 1, prv = cur ^ 1;
-  const T* G = static_cast<const T*>(R.g);
   T* Yw = static_cast<T*>(R.y);
   T* X1 = static_cast<T*>(R.x1);
   T* S = static_cast<T*>(R.save);
   float* hs_cur = R.hs + (long)cur * a.B * H;
-  const float* hs_prv = R.hs + (long)prv * a.B * H;
   const __amdgpu_buffer_rsrc_t srs = tt_rsrc(S + ((long)m0 * T_ + t) * (4L * H));
   const __amdgpu_buffer_rsrc_t xrs = tt_rsrc(X1 ? X1 + ((long)m0 * T_ + t) * a.ldy : Yw);
   for (int hf = 0; hf < BMR / 64; ++hf) {
@@ -2000,8 +2011,12 @@ extern "C" int tt_gru_fwd(int dtype, const tt_gru_fwd_rec* recs, int nrec, int B
   if (bmr == 256 && 256L * span >= (1L << 31)) bmr = 128;
   TT_CHECK_ARG((long)bmr * span < (1L << 31), "tt_gru_fwd: tile byte offsets exceed 2 GiB (B tile %d)", bmr);
   dim3 grid(tt_ceil_div(H, 64) * tt_ceil_div(B, bmr) * nrec);
-  // 128-row tiles: a 3-stage product ring when option gru_step_ring >= 3 (120 KiB of LDS)
-  const bool ring = tt::opt(tt::OPT_GRU_STEP_RING) >= 3;
+  // 128-row tiles: a 3-stage product ring when option gru_step_ring >= 3 and the grid is
+  // one workgroup per CU at most (120 KiB of LDS: at two per CU the second workgroup's
+  // overlap is worth more, configs[4] 49.7 vs 85.9 ms per layer, profiles/r04_gru_fwd_ring_c4_s.txt)
+  XcDev* xd = nullptr;
+  TT_PROPAGATE(xc_device(&xd));
+  const bool ring = tt::opt(tt::OPT_GRU_STEP_RING) >= 3 && (long)grid.x <= xd->cus;
   for (int s = 0; s < T; ++s) {
     a.s = s;
     if (dtype == TT_DT_BF16) {
@@ -2090,7 +2105,13 @@ extern "C" int tt_gru_bwd(int dtype, const tt_gru_bwd_rec* recs, int nrec, int B
     TT_CHECK_HIP(hipEventRecord(side->fork, st));
     TT_CHECK_HIP(hipStreamWaitEvent(side->s, side->fork, 0));
   }
-  const int ring = tt::opt(tt::OPT_GRU_STEP_RING);
+  // the product ring (option gru_step_ring) where every chain's workgroups fit one per CU
+  // (96-128 KiB of LDS); otherwise two stages and up to two workgroups per CU
+  XcDev* xd = nullptr;
+  TT_PROPAGATE(xc_device(&xd));
+  long wgs = 0;
+  for (int g = 0; g < ngrp; ++g) wgs += (long)tt_ceil_div(H, 128) * tt_ceil_div(B, bmr) * gn[g];
+  const int ring = wgs <= xd->cus ? tt::opt(tt::OPT_GRU_STEP_RING) : 2;
   for (int s = T - 1; s >= 0; --s) {
     for (int g = 0; g < ngrp; ++g) {
       ga[g].s = s;

@@ -593,7 +593,10 @@ struct Loop8 {
     return;
 #endif
     int dt = 0;
-    if constexpr (L::SHIFTED) dt = (int)(((long)r * KTE) % ld.T_);
+    if constexpr (L::SHIFTED) {  // time advance of K-tile r: 32-bit, a mask when T is a power of two
+      const unsigned rk = (unsigned)r * (unsigned)KTE, tu = (unsigned)ld.T_;
+      dt = (int)((tu & (tu - 1u)) == 0u ? rk & (tu - 1u) : rk % tu);
+    }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       bool ok = r < pc[j].lim;

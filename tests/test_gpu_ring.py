@@ -11,7 +11,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _gru_once(dt, B, T, H, ring):
+def _gru_once(dt, B, T, H, ring, bwd_rows=0):
     """One per-step forward + backward over 4 recurrences (fp32: the per-step kernels)."""
     code = 0 if dt == torch.float32 else 1
     g = torch.Generator(device=DEV).manual_seed(71)
@@ -53,17 +53,19 @@ def _gru_once(dt, B, T, H, ring):
         r.dhstate = dhs[i].data_ptr()
         r.dbias_part = part[i].data_ptr()
         r.dir = d
-    with option("gru_step_ring", ring), option("gru_step", 1), option("gru_bwd_persist", 0):
+    with option("gru_step_ring", ring), option("gru_step", 1), option("gru_bwd_persist", 0), \
+            option("gru_bwd_rows", bwd_rows):
         call("tt_gru_fwd", code, recs, 4, B, T, H, 6 * H, 2 * H, 0.0, None, 0, st)
         call("tt_gru_bwd", code, brecs, 4, B, T, H, 2 * H, 8 * H, 0, st)
     torch.cuda.synchronize()
     return [y.clone() for y in Y] + [s.clone() for s in S] + [d.clone() for d in dG] + [p.clone() for p in part]
 
 
+@pytest.mark.parametrize("bwd_rows", [0, 128])  # 0: the host's pick (64-row tiles here)
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-def test_gru_step_ring_is_bit_identical(dt):
+def test_gru_step_ring_is_bit_identical(dt, bwd_rows):
     B, T, H = 256, 8, 256  # forward 4 x 2 x 4 = 32 workgroups, backward 2 x 4 x 2 x 2: one per CU
-    a = _gru_once(dt, B, T, H, 2)
-    b = _gru_once(dt, B, T, H, 4)
+    a = _gru_once(dt, B, T, H, 2, bwd_rows)
+    b = _gru_once(dt, B, T, H, 4, bwd_rows)
     for i, (x, y) in enumerate(zip(a, b)):
         assert torch.equal(x, y), i

@@ -1758,7 +1758,10 @@ bool gru_fwd_persistent(int dtype, int H) {
 static int bwd_rows(int B, int H, int nrec) {
   const int o = tt::opt(tt::OPT_GRU_BWD_ROWS);
   if (o == 64 || o == 128) return o;
-  return (long)tt_ceil_div(H, 128) * tt_ceil_div(B, 128) * nrec < 256 ? 64 : 128;
+  // 64-row tiles up to one 128-row workgroup per CU (fp32 B 2048, H 512: 9.93 ms per layer
+  // on 64-row tiles, two per CU, vs 12.48 on 128-row tiles with the product ring,
+  // profiles/r04_gru_bwd_rows_b2048_aa.txt)
+  return (long)tt_ceil_div(H, 128) * tt_ceil_div(B, 128) * nrec <= 256 ? 64 : 128;
 }
 // partial bias rows: one per backward row tile (the smallest tile: 64 rows; rows of a
 // larger-tile launch past its tile count are zero-filled by tt_gru_bwd and add nothing)

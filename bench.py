@@ -160,9 +160,10 @@ REGION_KERNEL = {"gru_bwd": ("gru_bwd_step<", "gru_bwd_big", "gru_bwd_rows<"), "
                  "embed_gather": ("embed_gather_kernel",)}
 
 
-def pmc_traffic(region, kernel, launches_per_step, args):
-    """HBM bytes per launch of the region's kernel from the committed PMC summary."""
-    key = (kernel,) if kernel and kernel != region else REGION_KERNEL.get(region)
+def pmc_traffic(region, kernels, launches_per_step, args):
+    """HBM bytes per launch of the region's kernels (every instance the region launched,
+    e.g. both layers' gru_fwd_xcp<H, DROP>) from the committed PMC summary."""
+    key = tuple(kernels) if kernels else REGION_KERNEL.get(region)
     if key is None or not os.path.exists(PMC_SUMMARY):
         return {"traffic": None, "traffic_source": "no PMC summary of this build committed"}
     # the committed PMC passes (tools/pmc_bench.sh) run the default configs[2] workload
@@ -353,7 +354,7 @@ def main():
 
     dom = max(kt, key=lambda k: kt[k]["ms_total"])
     roofline = {"kernel": kt[dom]["kernel"], "region": dom, **roof(dom),
-                **pmc_traffic(dom, kt[dom]["kernel"], kt[dom]["launches"] / max(args.steps, 1), args)}
+                **pmc_traffic(dom, kt[dom]["kernels"], kt[dom]["launches"] / max(args.steps, 1), args)}
     extra = {k: roof(k) for k in kt if k != dom}
     step_ms = 1e3 * elapsed / args.steps
     kernels = {k: {"kernel": v["kernel"], "ms_per_step": round(v["ms_total"] / args.steps, 3),

@@ -302,13 +302,16 @@ long tt_search_ws_size(int dtype, long Q, long N, int h, int k);
 int tt_margin_fwd(const float* qn, long bq, const float* dn, long nd, int h, long label_offset,
                   const int32_t* idx, int k, float margin, float* row_loss, void* stream);
 /* Gradient of g * sum_i row_loss_i: dqn (overwritten), ddn (accumulated; the caller
- * zeroes it). gscale: device pointer to g (as tt_infonce_bwd) or NULL for 1. ws: tt_margin_bwd_ws_size bytes (8 per row) or NULL; with it and
- * h <= 512, 64 (k + 1) <= 2048, repeated negatives are summed per 64-row group before
- * the atomics into ddn (hard negatives are shared by many rows). */
+ * zeroes it). gscale: device pointer to g (as tt_infonce_bwd) or NULL for 1.
+ * ws: tt_margin_bwd_ws_size(bq, nd, h, k) bytes (required). Deterministic: no float
+ * atomics; the rows are taken in groups of R (R (k + 1) <= 2048), each group sums the
+ * q rows of each document it mined in entry order, and each document's group partials
+ * are added in ascending group order (hard negatives are shared by many rows).
+ * 1 <= k < 2048. */
 int tt_margin_bwd(const float* qn, long bq, const float* dn, long nd, int h, long label_offset,
                   const int32_t* idx, int k, float margin, const float* gscale, float* dqn, float* ddn,
                   void* ws, void* stream);
-long tt_margin_bwd_ws_size(long bq);
+long tt_margin_bwd_ws_size(long bq, long nd, int h, int k);
 
 /* out[0] = scale * sum_i x[i]. */
 int tt_sum(const float* x, long n, float scale, float* out, void* stream);
@@ -317,10 +320,14 @@ int tt_sum(const float* x, long n, float scale, float* out, void* stream);
 /* torch.optim.Adam (train_enhanced.py:43,63) over up to 48 fp32 tensors per call,
  * bit-for-bit the update order of torch's single-tensor Adam:
  *   m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2 ;
- *   p -= lr/(1-b1^step) * m / (sqrt(v)/sqrt(1-b2^step) + eps)   (g += wd*p first). */
+ *   p -= lr/(1-b1^step) * m / (sqrt(v)/sqrt(1-b2^step) + eps)   (g += wd*p first).
+ * skip: device int32 word or NULL; when it reads non-zero at launch time the kernel
+ * changes nothing (p, m, v untouched). two_towers_amd.Adam passes the OR of the status
+ * words of the column-split forwards since the last step (tt_gru_fwd ws), so a step whose
+ * forward timed out cannot update the weights; no host synchronisation is involved. */
 int tt_adam_multi(float* const* params, const float* const* grads, float* const* exp_avg,
                   float* const* exp_avg_sq, const long* sizes, int ntensors, float lr, float beta1,
-                  float beta2, float eps, float weight_decay, int step, void* stream);
+                  float beta2, float eps, float weight_decay, int step, const int32_t* skip, void* stream);
 
 #ifdef __cplusplus
 }

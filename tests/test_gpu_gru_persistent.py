@@ -210,6 +210,34 @@ def test_column_split_member_timeout_is_reported_and_not_sticky():
         tta.check_gru_status()
     m(q, q)  # healthy again
     tta.check_gru_status()
+    # contained on the device: a timed-out forward's backward and Adam step leave every
+    # parameter and moment bit-unchanged (the step guard), although the host learns of the
+    # timeout only afterwards; the next healthy step trains normally
+    opt = tta.Adam(m.parameters(), lr=1e-2)
+    crit = tta.InfoNCELoss()
+    crit(*m(q, q)).backward()
+    opt.step()  # one healthy step, so the moments are non-zero
+    opt.zero_grad()
+    tta.check_gru_status()
+    before = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    moments = {id(p): (opt.state[p]["exp_avg"].clone(), opt.state[p]["exp_avg_sq"].clone()) for p in m.parameters()}
+    with option("gru_xc_spins", 14), option("gru_xc_skip", 1):
+        vq, vd = m(q, q)
+    crit(vq, vd).backward()
+    opt.step()
+    torch.cuda.synchronize()
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, before[k]), k
+    for p in m.parameters():
+        assert torch.equal(opt.state[p]["exp_avg"], moments[id(p)][0])
+        assert torch.equal(opt.state[p]["exp_avg_sq"], moments[id(p)][1])
+    with pytest.raises(tta.GruTimeoutError):
+        tta.check_gru_status()
+    opt.zero_grad()
+    crit(*m(q, q)).backward()
+    opt.step()
+    tta.check_gru_status()
+    assert any(not torch.equal(v, before[k]) for k, v in m.state_dict().items())
 
 
 @pytest.mark.parametrize("H,depth", [(64, 4), (128, 4), (128, 1), (192, 4), (256, 2), (320, 4), (384, 4), (448, 4),

@@ -172,7 +172,7 @@ def test_margin_bwd_repeated_negatives(B, nd, h, k, lab, hot):
     """tt_margin_bwd against float64 autograd of the reference rule
     (enhanced_two_tower.py:102-121 on normalised rows), with negatives repeated across
     rows (hot: a handful of documents mined by every row) or spread out. k = 40 takes
-    the per-row atomic kernel."""
+    16-row groups; two runs are bit-identical."""
     g = torch.Generator().manual_seed(B * 13 + k)
     q = torch.nn.functional.normalize(torch.randn(B, h, generator=g), dim=1)
     d = torch.nn.functional.normalize(torch.randn(nd, h, generator=g), dim=1)
@@ -185,14 +185,30 @@ def test_margin_bwd_repeated_negatives(B, nd, h, k, lab, hot):
     qd, dd, idd = q.to(DEV), d.to(DEV), idx.to(DEV)
     gdev = torch.tensor([gscale], dtype=torch.float32, device=DEV)  # device-side upstream gradient
     dq = torch.empty(B, h, device=DEV)
-    for use_ws in (True, False):  # grouped kernels / per-row atomic kernel
+    outs = []
+    for rep in range(2):  # deterministic: two runs give the same bits
         ddn = torch.zeros(nd, h, device=DEV)
-        ws = torch.empty(_lib.load().tt_margin_bwd_ws_size(B), dtype=torch.uint8, device=DEV)
+        ws = torch.empty(_lib.load().tt_margin_bwd_ws_size(B, nd, h, k), dtype=torch.uint8, device=DEV)
+        ws.fill_(0xA5 if rep else 0x5A)  # no result may depend on the workspace's previous contents
         call("tt_margin_bwd", qd.data_ptr(), B, dd.data_ptr(), nd, h, lab, idd.data_ptr(), k, margin, gdev.data_ptr(),
-             dq.data_ptr(), ddn.data_ptr(), ws.data_ptr() if use_ws else None, torch.cuda.current_stream().cuda_stream)
+             dq.data_ptr(), ddn.data_ptr(), ws.data_ptr(), torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         assert (dq.cpu().double() - rq).abs().max() < 1e-6
         assert (ddn.cpu().double() - rd).abs().max() < 1e-5 * float(rd.abs().max()) + 1e-7
+        outs.append(ddn.cpu())
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_margin_bwd_requires_workspace():
+    """The document gradient is summed through caller scratch: a null workspace is an
+    argument error, not a silent fallback."""
+    B, nd, h, k = 8, 16, 64, 2
+    q = torch.zeros(B, h, device=DEV)
+    d = torch.zeros(nd, h, device=DEV)
+    idx = torch.zeros(B, k, dtype=torch.int32, device=DEV)
+    with pytest.raises(RuntimeError, match="workspace"):
+        call("tt_margin_bwd", q.data_ptr(), B, d.data_ptr(), nd, h, 0, idx.data_ptr(), k, 0.2, None,
+             q.data_ptr(), d.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
 
 
 # ---------------------------------------------------------------- configs[3] per-rank shape

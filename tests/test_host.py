@@ -120,7 +120,7 @@ def test_bad_arguments_are_reported_not_launched():
     rc = lib.tt_gemm(7, 0, 0, 0, 4, 4, 4, None, 1, 4, 4, 4, 1.0, 0, 0, 0, 0, 0.0, 1, None, None)
     assert rc == _lib.TT_EINVAL
     assert "dtype" in lib.tt_last_error().decode()
-    assert lib.tt_adam_multi(None, None, None, None, None, 0, 1e-3, 0.9, 0.999, 1e-8, 0.0, 0, None) == _lib.TT_EINVAL
+    assert lib.tt_adam_multi(None, None, None, None, None, 0, 1e-3, 0.9, 0.999, 1e-8, 0.0, 0, None, None) == _lib.TT_EINVAL
 
 
 def test_product_path_fails_loudly_without_gpu():

@@ -140,11 +140,11 @@ _SIGS = {
                               c_void_p, c_void_p]),
     "tt_margin_bwd": (c_int, [c_void_p, c_long, c_void_p, c_long, c_int, c_long, c_void_p, c_int, c_float,
                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "tt_margin_bwd_ws_size": (c_long, [c_long]),
+    "tt_margin_bwd_ws_size": (c_long, [c_long, c_long, c_int, c_int]),
     "tt_sum": (c_int, [c_void_p, c_long, c_float, c_void_p, c_void_p]),
     "tt_adam_multi": (c_int, [POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p),
                               POINTER(c_long), c_int, c_float, c_float, c_float, c_float, c_float, c_int,
-                              c_void_p]),
+                              c_void_p, c_void_p]),
 }
 
 EXPORTED = tuple(_SIGS)

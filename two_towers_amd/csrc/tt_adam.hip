@@ -15,6 +15,7 @@ struct AdamArgs {
   float* m[MAXT];
   float* v[MAXT];
   long start[MAXT + 1];  // prefix sums of sizes
+  const int* skip;       // device word: non-zero -> leave every tensor unchanged (or null)
   int nt;
   float b2, omb1, omb2, eps, wd, step_size, bc2_sqrt;
 };
@@ -24,6 +25,7 @@ struct AdamArgs {
 //   denom = exp_avg_sq.sqrt() / bias_correction2_sqrt + eps
 //   param.addcdiv_(exp_avg, denom, value=-lr/bias_correction1)
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
+  if (a.skip && *a.skip != 0) return;  // an invalid forward fed this step
   const long e0 = (long)blockIdx.x * CHUNK;
   const long total = a.start[a.nt];
   int t = 0;
@@ -50,7 +52,8 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
 
 extern "C" int tt_adam_multi(float* const* params, const float* const* grads, float* const* exp_avg,
                              float* const* exp_avg_sq, const long* sizes, int ntensors, float lr, float beta1,
-                             float beta2, float eps, float weight_decay, int step, void* stream) {
+                             float beta2, float eps, float weight_decay, int step, const int32_t* skip,
+                             void* stream) {
   TT_CHECK_ARG(ntensors >= 0 && ntensors <= MAXT, "tt_adam_multi: at most %d tensors per call", MAXT);
   TT_CHECK_ARG(step >= 1, "tt_adam_multi: step must be >= 1");
   if (ntensors == 0) return 0;
@@ -64,6 +67,7 @@ extern "C" int tt_adam_multi(float* const* params, const float* const* grads, fl
     a.start[i + 1] = a.start[i] + sizes[i];
   }
   a.nt = ntensors;
+  a.skip = skip;
   a.b2 = beta2; a.omb1 = (float)(1.0 - (double)beta1); a.omb2 = (float)(1.0 - (double)beta2);
   a.eps = eps; a.wd = weight_decay;
   const double bc1 = 1.0 - pow((double)beta1, step);

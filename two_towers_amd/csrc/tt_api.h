@@ -37,7 +37,7 @@ enum Opt {
                         // (default 14, about half a step at configs[2]: 7.05-7.09 vs 7.49-7.54 ms per launch)
   OPT_GRU_FWD_SKEW,     // gru_fwd_xcp: start delay (s_sleep 127 units) of the odd groups
   OPT_GEMM_BRES,        // 0: no B-resident short-K GEMM (layer-0 input projection)
-  OPT_GRU_XC_COOP,      // 0: column-split forward by a plain launch (occupancy-checked) instead of a cooperative one
+  OPT_GRU_XC_COOP,      // 1: column-split forward by hipLaunchCooperativeKernel (default 0: a plain, occupancy-checked launch)
   OPT_GEMM_BUF,         // 0: 256x256 GEMM operand DMAs through per-lane pointers instead of buffer resources
   OPT_GEMM_ORDER,       // 1: persistent GEMM tiles in column groups per XCD
   OPT_GRU_STEP_RING,    // LDS stages of the per-step GRU kernels' product (2: double buffer; fwd uses <= 3)

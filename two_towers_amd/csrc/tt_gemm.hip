@@ -38,7 +38,7 @@ constexpr OptDef kOpts[OPT_N] = {
     {"gru_fwd_xc", "TT_GRU_FWD_XC", 1},           {"gru_xc_skip", "TT_GRU_XC_SKIP", 0},
     {"gru_xc_spins", "TT_GRU_XC_SPINS", 22},      {"gru_bwd_skew", "TT_GRU_BWD_SKEW", 14},
     {"gru_fwd_skew", "TT_GRU_FWD_SKEW", 0},       {"gemm_bres", "TT_GEMM_BRES", 1},
-    {"gru_xc_coop", "TT_GRU_XC_COOP", 1},         {"gemm_buf", "TT_GEMM_BUF", 1},
+    {"gru_xc_coop", "TT_GRU_XC_COOP", 0},         {"gemm_buf", "TT_GEMM_BUF", 1},
     {"gemm_order", "TT_GEMM_ORDER", 0},           {"gru_step_ring", "TT_GRU_STEP_RING", 4},
 };
 struct OptTable {
@@ -956,7 +956,10 @@ int launch_gemm(int akout, int bkout, bool shift, GemmArgs& g, int nbatch, hipSt
   {
     const long span = (long)(g.kt_per_split + 2) * (ttg::KTB / (int)sizeof(T)) * (long)sizeof(T);
     if (akout && span * g.lda >= (1L << 32)) buf = false;
-    if (bkout && !shift && span * g.ldb >= (1L << 32)) buf = false;
+    if (bkout && span * g.ldb >= (1L << 32)) buf = false;
+    // the shifted operand's buffer form (Loop8 SHalf) masks one k-row per sequence
+    // boundary: it needs T to be a whole number of K-tiles
+    if (shift && g.seq_t % (ttg::KTB / (int)sizeof(T)) != 0) buf = false;
     if (!akout && (long)256 * g.lda * (long)sizeof(T) >= (1L << 31)) buf = false;
     if (!bkout && (long)256 * g.ldb * (long)sizeof(T) >= (1L << 31)) buf = false;
     for (int b = 0; b < 4 && g.a_split > 0; ++b) {
@@ -965,7 +968,7 @@ int launch_gemm(int akout, int bkout, bool shift, GemmArgs& g, int nbatch, hipSt
       if (d < 0 || d + (g.M - g.a_split) > g.lda) buf = false;
     }
   }
-  if (dma && persist_ok && (g.force_regstage == 0 || g.force_regstage >= 9) && g.splits == 1 && !g.beta && nk >= 2 && nk <= tt::opt(tt::OPT_GEMM_PERSIST_MAXK) && t256 >= 512 &&
+  if (dma && persist_ok && !shift && (g.force_regstage == 0 || g.force_regstage >= 9) && g.splits == 1 && !g.beta && nk >= 2 && nk <= tt::opt(tt::OPT_GEMM_PERSIST_MAXK) && t256 >= 512 &&
       use_big(g.M, g.N, t256))
     return launch_persist<T, TO>(akout, bkout, shift, g, (int)t256, buf, st);
   if (dma && g.force_regstage != 2 && use_big(g.M, g.N, t256)) {

@@ -681,15 +681,90 @@ struct Loop8 {
       delta = KO ? (long)KTE * l.ld * (long)sizeof(T) : (long)KTB;
     }
     TT_DEV void issue(int r, uint32_t img) const { issue_half(ld, pc, r, delta, img); }
+    TT_DEV void fix(int, uint32_t) const {}
   };
   template <bool KO, class L>
   struct BHalf {
     BufHalf h;
     TT_DEV void init(const L& l, int kt0, int ktl, int K, int roff) { init_buf<KO>(l, kt0, K, roff, h); }
     TT_DEV void issue(int r, uint32_t img) const { issue_buf(h, r, img); }
+    TT_DEV void fix(int, uint32_t) const {}
+  };
+  // BUF form of the time-shifted K-outer operand (KOShift, dW_hh's h_{s-1}) for T a
+  // multiple of the K-tile depth: every piece reads the K-tile's own k-rows moved by
+  // `shift` rows, so the pieces keep fixed per-lane offsets and the K-tile advance stays an
+  // SGPR (no per-piece time arithmetic or source select). The one k-row per masked K-tile
+  // whose time index t has t + shift outside [0, T) (k-row 0 for shift -1 when t = 0,
+  // k-row KTE-1 for shift +1 when t = T-1) then holds a neighbouring sequence's row; the
+  // lanes that DMA'd it overwrite it with zeros in LDS after the wait that retires the
+  // K-tile (fix), before the barrier that precedes its first fragment read. Every lane
+  // stays in range (out-of-range lanes slow the whole DMA instruction down: DESIGN.md §3)
+  // except the operand's very last K-tile under shift +1, whose row K reads zero through
+  // num_records. Shift -1 at the operand's first K-tile would read row -1: that K-tile's
+  // masked lanes read row 0 instead (voff0), which fix zeroes as well.
+  template <bool KO, class L>
+  struct SHalf {
+    BufHalf h;
+    uint32_t voff0[2];  // relative K-tile 0
+    int kt0, tkt;       // first K-tile, K-tiles per sequence
+    int klm;            // masked k-row: 0 (shift -1) or KTE-1 (shift +1)
+    bool zl[2];         // this lane DMA'd the masked k-row in piece j
+    bool zany;          // ... in either piece, for some lane of this wave (wave-uniform)
+    TT_DEV void init(const L& l, int kt0_, int ktl, int K, int roff) {
+      static_assert(KO, "time-shifted operands are K-outer");
+      const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+      kt0 = kt0_;
+      tkt = l.T_ / KTE;
+      klm = l.shift < 0 ? 0 : KTE - 1;
+      const long k0 = (long)kt0 * KTE;
+      long nrec = ((long)K - k0 - l.shift) * l.ld * (long)sizeof(T);
+      nrec = nrec < 0 ? 0 : (nrec > 0xFFFFFFFFL ? 0xFFFFFFFFL : nrec);
+      h.rs = make_rsrc4(l.base + (k0 + l.shift) * l.ld, (uint32_t)nrec);
+      h.delta = (uint32_t)((long)KTE * l.ld * (long)sizeof(T));
+      constexpr int CPR = 128 * (int)sizeof(T) / 16;
+      bool any = false;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int p = (wave + 8 * j) * 64 + lane;
+        const int kl = p / CPR, q = p % CPR;
+        int c;
+        if constexpr (sizeof(T) == 2) c = q ^ (ko_v(kl) << 1);
+        else c = q ^ (((kl >> 2) & 1) << 2);
+        const long col = (long)l.c0 + roff + c * Elt<T>::EPC;
+        h.voff[j] = (uint32_t)(((long)kl * l.ld + col) * (long)sizeof(T));
+        zl[j] = kl == klm;
+        any |= zl[j];
+        // shift -1 from the operand's first K-tile: k-row 0 would be row -1
+        voff0[j] = (zl[j] && kt0 == 0 && l.shift < 0) ? (uint32_t)((l.ld + col) * (long)sizeof(T)) : h.voff[j];
+      }
+      zany = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_ballot_w64(any) != 0 ? 1 : 0) != 0;
+    }
+    TT_DEV void issue(int r, uint32_t img) const {
+      const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+      const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)r * h.delta);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) dma16_buf(h.rs, r == 0 ? voff0[j] : h.voff[j], soff, img + (uint32_t)(wave + 8 * j) * 1024u);
+    }
+    // after this wave's wait that retired relative K-tile r (image img): zero the masked
+    // k-row if K-tile r has one; ordered before the next barrier by lgkmcnt(0)
+    TT_DEV void fix(int r, uint32_t img) const {
+      const int kt = kt0 + r;
+      const bool masked = (klm == 0 ? kt : kt + 1) % tkt == 0;
+      if (!zany || !masked) return;
+      const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        if (zl[j]) {
+          const uint32_t a = img + (uint32_t)(wave + 8 * j) * 1024u + (uint32_t)lane * 16u;
+          const tt_rsrc4 z = {0u, 0u, 0u, 0u};
+          asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(z) : "memory");
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
   };
   template <bool KO, class L>
-  using Half = std::conditional_t<BUF && !L::SHIFTED && !L::KSPLIT, BHalf<KO, L>, PHalf<KO, L>>;
+  using Half = std::conditional_t<BUF && !L::KSPLIT, std::conditional_t<L::SHIFTED, SHalf<KO, L>, BHalf<KO, L>>,
+                                  PHalf<KO, L>>;
 
   TT_DEV static void quad(int mi, int ni, const uint4 (&fa)[2][4], const uint4 (&fb)[2][4], f32x4 (&acc)[TM][TN]) {
     __builtin_amdgcn_s_barrier();
@@ -729,6 +804,8 @@ struct Loop8 {
     pb0.issue(1, base + SLOT + 2 * HALF);
     pb1.issue(1, base + SLOT + 3 * HALF);
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    pb0.fix(0, base + 2 * HALF);
+    pb1.fix(0, base + 3 * HALF);
     __builtin_amdgcn_s_barrier();
     const bool late = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;  // wave row 1
     if (late) __builtin_amdgcn_s_barrier();
@@ -765,6 +842,8 @@ struct Loop8 {
         pb0.issue(r + 2, cur + 2 * HALF);
         pb1.issue(r + 2, cur + 3 * HALF);
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        pb0.fix(r + 1, nxt + 2 * HALF);
+        pb1.fix(r + 1, nxt + 3 * HALF);
         quad(1, 0, fa, fb, acc);
         continue;
       }
@@ -791,6 +870,8 @@ struct Loop8 {
       // P4
       pb1.issue(r + 2, cur + 3 * HALF);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      pb0.fix(r + 1, nxt + 2 * HALF);
+      pb1.fix(r + 1, nxt + 3 * HALF);
       quad(1, 0, fa, fb, acc);
     }
     if (!late) __builtin_amdgcn_s_barrier();  // re-align the two wave rows
@@ -816,6 +897,8 @@ struct Loop8 {
     pb0.issue(1, base + BOFF + 2 * HALF);
     pb1.issue(1, base + BOFF + 3 * HALF);
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    pb0.fix(0, base + BOFF);
+    pb1.fix(0, base + BOFF + HALF);
     __builtin_amdgcn_s_barrier();
     const bool late = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;  // wave row 1
     if (late) __builtin_amdgcn_s_barrier();
@@ -850,6 +933,11 @@ struct Loop8 {
       pb0.issue(r + 2, bcur);
       pb1.issue(r + 2, bcur + HALF);
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      {  // K-tile r+1 (B slot (r+1) & 1) has landed for this wave's DMAs
+        const uint32_t bnx = base + BOFF + (uint32_t)(bs ^ 1) * (2 * HALF);
+        pb0.fix(r + 1, bnx);
+        pb1.fix(r + 1, bnx + HALF);
+      }
       quad(1, 0, fa, fb, acc);
       as = as == 2 ? 0 : as + 1;
     }

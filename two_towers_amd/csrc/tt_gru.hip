@@ -1936,8 +1936,13 @@ static int gru_fwd_xc_launch(const FwdArgs& a, int nrec, int B, int T, int H, lo
   void* args[] = {&ak, &wk};
   const void* fn = H == 512 ? (drop ? xc_kernel<512, true>() : xc_kernel<512, false>())
                             : (drop ? xc_kernel<256, true>() : xc_kernel<256, false>());
-  // cooperative: the runtime checks the grid against the co-residency limit at launch
-  // (option gru_xc_coop 0: a plain launch, guarded by xc_plan's occupancy check only)
+  // A plain launch by default: xc_plan has already checked the grid (<= one workgroup per
+  // CU) against the occupancy query, which is all a cooperative launch checks on gfx950
+  // (MI355X_MICROARCH.md "coop-launch": same residency, +15-19 us per launch), and the
+  // member waits are bounded (status word -> GruTimeoutError, Adam step guard). Option
+  // gru_xc_coop 1 restores hipLaunchCooperativeKernel; under rocprofv3 that form made the
+  // profiled process fault in teardown after the profiler's finalisation
+  // (profiles/r04_rocprof_crash_k.txt), the plain one does not.
   const hipError_t e = tt::opt(tt::OPT_GRU_XC_COOP)
                            ? hipLaunchCooperativeKernel(fn, dim3(g.grid), dim3(xc::NT), args, 0, st)
                            : hipLaunchKernel(fn, dim3(g.grid), dim3(xc::NT), args, 0, st);

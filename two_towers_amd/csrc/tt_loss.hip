@@ -427,54 +427,28 @@ __global__ __launch_bounds__(256) void margin_fwd_kernel(const float* __restrict
   if (lane == 0) row_loss[row] = fmaxf(margin - pos + neg, 0.f);
 }
 
-__global__ __launch_bounds__(256) void margin_bwd_kernel(const float* __restrict__ qn, long bq,
-                                                         const float* __restrict__ dn, int h, long label_off,
-                                                         const int32_t* __restrict__ idx, int k, float margin,
-                                                         const float* __restrict__ gscale, float* __restrict__ dqn,
-                                                         float* __restrict__ ddn) {
-  const float gs = gscale ? *gscale : 1.f;
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (row >= bq) return;
-  const float* q = qn + row * h;
-  const long lab = label_off + row;
-  const float* dp = dn + lab * h;
-  float pos = 0.f, neg = 0.f;
-  for (int c = lane; c < h; c += 64) pos += q[c] * dp[c];
-  for (int j = 0; j < k; ++j) {
-    const float* dj = dn + (long)idx[row * k + j] * h;
-    for (int c = lane; c < h; c += 64) neg += q[c] * dj[c];
-  }
-  pos = wave_sum(pos);
-  neg = wave_sum(neg) / k;
-  // torch.clamp(min=0) passes the gradient where the argument is >= 0
-  const bool active = (margin - pos + neg) >= 0.f;
-  const float gn = active ? gs / k : 0.f;
-  const float gp = active ? -gs : 0.f;
-  for (int c = lane; c < h; c += 64) {
-    float d = gp * dp[c];
-    for (int j = 0; j < k; ++j) d += gn * dn[(long)idx[row * k + j] * h + c];
-    dqn[row * h + c] = d;
-  }
-  if (active) {
-    for (int c = lane; c < h; c += 64) {
-      atomicAdd(ddn + lab * h + c, gp * q[c]);
-      for (int j = 0; j < k; ++j) atomicAdd(ddn + (long)idx[row * k + j] * h + c, gn * q[c]);
-    }
-  }
-}
+// Backward in three launches, deterministic (the same inputs give the same bits in every
+// run: no float atomics; the document gradient of every document is summed in a fixed
+// order). Mined negatives repeat across rows (rows of one batch share their hardest
+// documents), so the document sums go through groups of R rows:
+//   margin_rows_kernel    : one wave per row (all rows in flight): dqn and the row's
+//                           coefficients (positive -gscale, each negative gscale / k; 0
+//                           when the hinge is inactive);
+//   margin_group_kernel   : one workgroup per R rows (R (k + 1) <= 2048 entries): the
+//                           group's (document, entry) keys sorted in LDS (bitonic), slots
+//                           numbered in sorted order, one coefficient-weighted sum of q rows
+//                           per distinct document in entry order -> partial row P[g][slot];
+//                           slot map SM[document][g] = slot + 1 (0: the group has none);
+//   margin_combine_kernel : one wave per document: the partials of the groups that hold
+//                           it, in ascending group order, then ddn[document] += the sum.
+constexpr int MB_ENT = 2048;
 
-// Batched form (h <= 512, 64 * (k + 1) <= 2048): mined negatives repeat across rows
-// (rows of one batch share their hardest documents), so per-element atomics straight
-// from every row pile up on a few ddn rows. Two launches instead:
-//   margin_rows_kernel : one wave per row (all rows in flight): dqn and the row's
-//                        coefficients (positive -gscale, each negative gscale / k; 0 when
-//                        the hinge is inactive);
-//   margin_ddn_kernel  : one workgroup per 64 rows: its q rows staged in LDS, its
-//                        (document, entry) keys sorted by document (bitonic, 2048 keys),
-//                        then one coefficient-weighted sum of q rows per distinct
-//                        document and one atomic per (workgroup, document, element).
-constexpr int MB_ROWS = 64, MB_ENT = 2048, MB_HMAX = 512;
+// rows per group: the largest power of two <= 64 with R (k + 1) <= MB_ENT
+inline int margin_group_rows(int k) {
+  int r = 64;
+  while (r > 1 && (long)r * (k + 1) > MB_ENT) r >>= 1;
+  return r;
+}
 
 __global__ __launch_bounds__(256) void margin_rows_kernel(const float* __restrict__ qn, long bq,
                                                           const float* __restrict__ dn, int h, long label_off,
@@ -507,35 +481,35 @@ __global__ __launch_bounds__(256) void margin_rows_kernel(const float* __restric
   if (lane == 0) coef[row] = make_float2(gp, gn);
 }
 
-__global__ __launch_bounds__(256) void margin_ddn_kernel(const float* __restrict__ qn, long bq, int h, long label_off,
-                                                         const int32_t* __restrict__ idx, int k,
-                                                         const float2* __restrict__ coef,
-                                                         float* __restrict__ ddn) {
+__global__ __launch_bounds__(256) void margin_group_kernel(const float* __restrict__ qn, long bq, int h,
+                                                           long label_off, const int32_t* __restrict__ idx, int k,
+                                                           const float2* __restrict__ coef, int R, int G,
+                                                           float* __restrict__ P, int* __restrict__ SM) {
   __shared__ unsigned long long key[MB_ENT];  // document << 32 | entry; unused = all ones
-  __shared__ float2 cf[MB_ROWS];
-  __shared__ int heads[MB_ENT];
-  __shared__ int nheads;
-  __shared__ __attribute__((aligned(16))) float qs[MB_ROWS * MB_HMAX];
-  const long r0 = (long)blockIdx.x * MB_ROWS;
-  const int nr = (int)(bq - r0 < MB_ROWS ? bq - r0 : MB_ROWS);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __shared__ int head[MB_ENT];                // sorted position of slot u's first entry
+  __shared__ int wsum[256];
+  const int g = blockIdx.x;
+  const long r0 = (long)g * R;
+  const int nr = (int)(bq - r0 < R ? bq - r0 : R);
   const int kp = k + 1;  // entry 0 of a row: its positive; 1..k: its negatives
-  for (int e = threadIdx.x; e < MB_ENT; e += 256) key[e] = ~0ull;
-  for (int e = threadIdx.x; e < nr * h; e += 256) qs[e] = qn[r0 * h + e];
-  if (threadIdx.x < MB_ROWS) cf[threadIdx.x] = threadIdx.x < nr ? coef[r0 + threadIdx.x] : make_float2(0.f, 0.f);
-  if (threadIdx.x == 0) nheads = 0;
-  __syncthreads();
-  for (int e = threadIdx.x; e < nr * kp; e += 256) {
-    const int rl = e / kp, j = e - rl * kp;
-    if (cf[rl].x != 0.f) {
-      const long doc = j == 0 ? label_off + r0 + rl : (long)idx[(r0 + rl) * k + j - 1];
-      key[e] = ((unsigned long long)doc << 32) | (unsigned)e;
+  const int ne = nr * kp;
+  int n2 = 2;
+  while (n2 < ne) n2 <<= 1;
+  for (int e = threadIdx.x; e < n2; e += 256) {
+    unsigned long long v = ~0ull;
+    if (e < ne) {
+      const int rl = e / kp, j = e - rl * kp;
+      if (coef[r0 + rl].x != 0.f) {
+        const long doc = j == 0 ? label_off + r0 + rl : (long)idx[(r0 + rl) * k + j - 1];
+        v = ((unsigned long long)doc << 32) | (unsigned)e;
+      }
     }
+    key[e] = v;
   }
   __syncthreads();
-  for (int size = 2; size <= MB_ENT; size <<= 1) {  // bitonic sort, ascending
+  for (int size = 2; size <= n2; size <<= 1) {  // bitonic sort, ascending
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int t = threadIdx.x; t < MB_ENT / 2; t += 256) {
+      for (int t = threadIdx.x; t < n2 / 2; t += 256) {
         const int i = 2 * t - (t & (stride - 1));
         const int j = i + stride;
         const bool up = (i & size) == 0;
@@ -545,34 +519,105 @@ __global__ __launch_bounds__(256) void margin_ddn_kernel(const float* __restrict
       __syncthreads();
     }
   }
-  for (int i = threadIdx.x; i < MB_ENT; i += 256) {
+  // slots in sorted order: thread t owns positions [t * per, (t + 1) * per)
+  const int per = (n2 + 255) / 256;
+  const int p0 = threadIdx.x * per;
+  int cnt = 0;
+  for (int i = p0; i < p0 + per && i < n2; ++i) {
     const unsigned long long v = key[i];
-    if (v != ~0ull && (i == 0 || (key[i - 1] >> 32) != (v >> 32))) heads[atomicAdd(&nheads, 1)] = i;
+    cnt += v != ~0ull && (i == 0 || (key[i - 1] >> 32) != (v >> 32));
+  }
+  wsum[threadIdx.x] = cnt;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {  // inclusive scan of the per-thread counts
+    const int add = threadIdx.x >= off ? wsum[threadIdx.x - off] : 0;
+    __syncthreads();
+    wsum[threadIdx.x] += add;
+    __syncthreads();
+  }
+  int u = wsum[threadIdx.x] - cnt;
+  for (int i = p0; i < p0 + per && i < n2; ++i) {
+    const unsigned long long v = key[i];
+    if (v != ~0ull && (i == 0 || (key[i - 1] >> 32) != (v >> 32))) head[u++] = i;
   }
   __syncthreads();
-  const int nh = nheads;
-  for (int u = wave; u < nh; u += 4) {
-    const int i0 = heads[u];
+  const int nh = wsum[255];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float* Pg = P + (long)g * R * kp * h;
+  for (int s = wave; s < nh; s += 4) {
+    const int i0 = head[s];
     const unsigned doc = (unsigned)(key[i0] >> 32);
     for (int c0 = 0; c0 < h; c0 += 256) {
       float acc[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int i = i0; i < MB_ENT && key[i] != ~0ull && (unsigned)(key[i] >> 32) == doc; ++i) {
+      for (int i = i0; i < n2 && key[i] != ~0ull && (unsigned)(key[i] >> 32) == doc; ++i) {
         const int e = (int)(key[i] & 0xffffffffu);
         const int rl = e / kp;
-        const float w = e - rl * kp == 0 ? cf[rl].x : cf[rl].y;
+        const float w = e - rl * kp == 0 ? coef[r0 + rl].x : coef[r0 + rl].y;
+        const float* q = qn + (r0 + rl) * h;
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const int c = c0 + lane + 64 * m;
-          if (c < h) acc[m] += w * qs[rl * h + c];
+          if (c < h) acc[m] += w * q[c];
         }
       }
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const int c = c0 + lane + 64 * m;
-        if (c < h) atomicAdd(ddn + (long)doc * h + c, acc[m]);
+        if (c < h) Pg[(long)s * h + c] = acc[m];
       }
     }
+    if (lane == 0) SM[(long)doc * G + g] = s + 1;
   }
+}
+
+__global__ __launch_bounds__(256) void margin_combine_kernel(const int* __restrict__ SM, int G,
+                                                             const float* __restrict__ P, long gstride, int h,
+                                                             long nd, float* __restrict__ ddn) {
+  const long doc = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (doc >= nd) return;
+  const int* sm = SM + doc * G;
+  bool any = false;
+  for (int g0 = 0; g0 < G; g0 += 64) any |= __builtin_amdgcn_ballot_w64(g0 + lane < G && sm[g0 + lane] != 0) != 0;
+  if (!any) return;
+  for (int c0 = 0; c0 < h; c0 += 256) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int g0 = 0; g0 < G; g0 += 64) {
+      const int s = g0 + lane < G ? sm[g0 + lane] : 0;
+      unsigned long long mask = __builtin_amdgcn_ballot_w64(s != 0);
+      while (mask) {  // groups in ascending order
+        const int b = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        const int slot = __builtin_amdgcn_readlane(s, b) - 1;
+        const float* p = P + (long)(g0 + b) * gstride + (long)slot * h;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int c = c0 + lane + 64 * m;
+          if (c < h) acc[m] += p[c];
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int c = c0 + lane + 64 * m;
+      if (c < h) ddn[doc * h + c] += acc[m];
+    }
+  }
+}
+
+struct MarginWs {
+  int R, G;
+  long off_sm, off_p, bytes;
+};
+inline MarginWs margin_ws(long bq, long nd, int h, int k) {
+  auto al = [](long x) { return (x + 255) & ~255L; };
+  MarginWs w{};
+  w.R = margin_group_rows(k);
+  w.G = (int)((bq + w.R - 1) / w.R);
+  w.off_sm = al(bq * 8);
+  w.off_p = w.off_sm + al(nd * w.G * 4);
+  w.bytes = w.off_p + al((long)w.G * w.R * (k + 1) * h * 4);
+  return w;
 }
 
 inline int esize(int dtype) { return dtype == TT_DT_BF16 ? 2 : 4; }
@@ -807,25 +852,33 @@ extern "C" int tt_margin_fwd(const float* qn, long bq, const float* dn, long nd,
   return 0;
 }
 
-extern "C" long tt_margin_bwd_ws_size(long bq) { return bq > 0 ? bq * 8 : 8; }
+extern "C" long tt_margin_bwd_ws_size(long bq, long nd, int h, int k) {
+  if (bq <= 0 || k < 1) return 256;
+  return margin_ws(bq, nd, h, k).bytes;
+}
 
 extern "C" int tt_margin_bwd(const float* qn, long bq, const float* dn, long nd, int h, long label_offset,
                              const int32_t* idx, int k, float margin, const float* gscale, float* dqn, float* ddn,
                              void* ws, void* stream) {
-  TT_CHECK_ARG(label_offset >= 0 && label_offset + bq <= nd && k >= 1, "tt_margin_bwd: bad labels/k");
+  TT_CHECK_ARG(label_offset >= 0 && label_offset + bq <= nd && k >= 1 && k < MB_ENT, "tt_margin_bwd: bad labels/k");
+  TT_CHECK_ARG(nd < (1L << 31), "tt_margin_bwd: nd=%ld too large", nd);
   if (bq == 0) return 0;
-  if ((long)MB_ROWS * (k + 1) <= MB_ENT && h <= MB_HMAX && nd < (1L << 31) && ws) {
-    float2* coef = static_cast<float2*>(ws);
-    hipLaunchKernelGGL(margin_rows_kernel, dim3((unsigned)tt_ceil_div(bq, 4)), dim3(256), 0, (hipStream_t)stream, qn,
-                       bq, dn, h, label_offset, idx, k, margin, gscale, dqn, coef);
-    TT_CHECK_LAUNCH("margin_rows_kernel");
-    hipLaunchKernelGGL(margin_ddn_kernel, dim3((unsigned)tt_ceil_div(bq, MB_ROWS)), dim3(256), 0, (hipStream_t)stream,
-                       qn, bq, h, label_offset, idx, k, coef, ddn);
-    TT_CHECK_LAUNCH("margin_ddn_kernel");
-    return 0;
-  }
-  hipLaunchKernelGGL(margin_bwd_kernel, dim3((unsigned)tt_ceil_div(bq, 4)), dim3(256), 0, (hipStream_t)stream, qn, bq,
-                     dn, h, label_offset, idx, k, margin, gscale, dqn, ddn);
-  TT_CHECK_LAUNCH("margin_bwd_kernel");
+  TT_CHECK_ARG(ws != nullptr, "tt_margin_bwd: null workspace (tt_margin_bwd_ws_size bytes)");
+  const MarginWs w = margin_ws(bq, nd, h, k);
+  char* base = static_cast<char*>(ws);
+  float2* coef = reinterpret_cast<float2*>(base);
+  int* SM = reinterpret_cast<int*>(base + w.off_sm);
+  float* P = reinterpret_cast<float*>(base + w.off_p);
+  hipStream_t st = (hipStream_t)stream;
+  TT_CHECK_HIP(hipMemsetAsync(SM, 0, nd * w.G * 4, st));
+  hipLaunchKernelGGL(margin_rows_kernel, dim3((unsigned)tt_ceil_div(bq, 4)), dim3(256), 0, st, qn, bq, dn, h,
+                     label_offset, idx, k, margin, gscale, dqn, coef);
+  TT_CHECK_LAUNCH("margin_rows_kernel");
+  hipLaunchKernelGGL(margin_group_kernel, dim3((unsigned)w.G), dim3(256), 0, st, qn, bq, h, label_offset, idx, k,
+                     coef, w.R, w.G, P, SM);
+  TT_CHECK_LAUNCH("margin_group_kernel");
+  hipLaunchKernelGGL(margin_combine_kernel, dim3((unsigned)tt_ceil_div(nd, 4)), dim3(256), 0, st, SM, w.G, P,
+                     (long)w.R * (k + 1) * h, h, nd, ddn);
+  TT_CHECK_LAUNCH("margin_combine_kernel");
   return 0;
 }

@@ -29,53 +29,21 @@
 
 namespace {
 
-// Timing-only diagnostic switches (`make exp EXP=-DHN_DIAG=n`; results are wrong):
-// 1 no tile DMAs after the first two, 2 no MFMAs, 4 no chunk-max epilogue, 8 no query loads
-#ifndef HN_DIAG
-#define HN_DIAG 0
-#endif
-#ifndef HN_PAIR_PREFETCH
-#define HN_PAIR_PREFETCH 1
-#endif
 constexpr int SC_COLS = 64;     // document columns per tile (= per chunk)
-#ifndef HN_W4
-#define HN_W4 1
-#endif
-#ifndef HN_PIPE_Q  // 1: query prologue overlapped with the first tile (measured no faster: profiles/r04_hn_scan_pipeq_h.txt)
-#define HN_PIPE_Q 0
-#endif
+constexpr int SC_RB = 2;        // 16-query MFMA blocks per wave
 constexpr int SC_TPS_MAX = 32;  // tiles per workgroup (chunk-max staging)
 
 // Per width (h = 32 KS). h <= 256: 8 waves (two per SIMD, 256 query rows per workgroup)
 // and a 4-slot LDS tile ring that travels in pairs. h 512: a tile is 64 KiB and the
 // query fragments alone are 128 registers per lane, so 4 waves (one per SIMD, 512
 // registers each, 128 query rows) and a 2-slot ring, one tile per barrier.
-// h 256 (HN_W4): 4 waves (one per SIMD) of 64 query rows each: every LDS fragment read
-// feeds 4 MFMAs, half the LDS read traffic of 8 waves x 32 rows (which the diagnostics put
-// at a quarter of the scan, profiles/r04_hn_scan_diag.txt), 256 rows per workgroup as before
 template <int KS>
 struct ScanCfg {
-  static constexpr bool W4 = KS == 8 && HN_W4;
-  static constexpr int WAVES = KS <= 8 && !W4 ? 8 : 4;
-  static constexpr int RB = W4 ? 4 : 2;  // 16-query MFMA blocks per wave
-  static constexpr int ROWS = WAVES * RB * 16;
+  static constexpr int WAVES = KS <= 8 ? 8 : 4;
+  static constexpr int ROWS = WAVES * SC_RB * 16;
   static constexpr int SLOTS = KS <= 8 ? 4 : 2;
 };
 
-// max of three scores in one v_max3_f32: fmaxf() would also quiet each input (an extra
-// v_max_f32 x, x per operand under the IEEE mode); the scores are finite
-TT_DEV float vmax3(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-// max of the 16 scores a lane holds for one query in a 64-document tile
-TT_DEV float max16(const float (&v)[16]) {
-  float m = vmax3(v[0], v[1], v[2]);
-#pragma unroll
-  for (int j = 3; j < 15; j += 2) m = vmax3(m, v[j], v[j + 1]);
-  return vmax3(m, v[15], v[15]);
-}
 // max over the four 16-lane rows of a wave (lanes l, l+16, l+32, l+48), result in all
 TT_DEV float rowgroup_max4(float v) {
   const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
@@ -145,7 +113,6 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
                                                                  float* __restrict__ CM, int map) {
   using TI = ScanTile<KS>;
   constexpr int SC_WAVES = ScanCfg<KS>::WAVES, SC_ROWS = ScanCfg<KS>::ROWS, SC_SLOTS = ScanCfg<KS>::SLOTS;
-  constexpr int SC_RB = ScanCfg<KS>::RB;
   // tile ring + chunk maxima [tile][row]: 4 x 32 KiB + 32 KiB (h 256) or 2 x 64 KiB + 16
   // KiB (h 512), one workgroup per CU
   __shared__ __attribute__((aligned(16))) char lds[SC_SLOTS * TI::BYTES + SC_TPS_MAX * SC_ROWS * 4];
@@ -154,9 +121,8 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
   // document slice in that L2; map 1 (option hn_map): the S splits of a row tile share an
   // XCD (xcd_remap), so the tile's query rows are fetched into that L2 once
   // map 2: XCD x (= b % 8) owns row-tile half x & 1 and split quarter x >> 1, so each XCD
-  // reads half of Q and a quarter of D (8 x 3 MB from HBM at 8192^2 x 256 instead of 8 x
-  // 4.5 MB: the query prologue, every CU at once, is HBM-bound); needs RT % 2 == 0 and
-  // S % 4 == 0 (the host falls back to map 0 otherwise)
+  // reads half of Q and a quarter of D (8 x 3 MB at 8192^2 x 256 instead of 8 x 4.5 MB);
+  // needs RT % 2 == 0 and S % 4 == 0 (the host falls back to map 0 otherwise)
   int split, rt;
   if (map == 2) {
     const int x = blockIdx.x & 7, j = blockIdx.x >> 3, sq = S >> 2;
@@ -173,42 +139,24 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const long row0 = (long)rt * SC_ROWS + wave * (SC_RB * 16);
   constexpr int h = 32 * KS;
-  // The first tiles are requested before the query rows, so their latency overlaps. With
-  // the 4-slot ring (PQ: the default h 256 form) all four slots are filled up front and the
-  // query fragments are loaded k-step by k-step after them and NOT retired here: tile 0's
-  // k-step ks waits (hipcc's own counted vmcnt) only for the fragments of k-steps <= ks,
-  // so the query prologue overlaps the first tile's MFMAs. The waits are exact: every DMA
-  // in flight then is older than the query loads, and none is issued before tile 2's
-  // barrier, by which time tile 0 has consumed every fragment.
+  // The first two tiles are requested before the query rows, so their latency overlaps.
   ScanDma<KS> dm;
   dm.init();
   const uint32_t lbase = __builtin_amdgcn_readfirstlane(ttg::lds_addr_of(lds));
-  constexpr bool PQ = SC_SLOTS == 4 && HN_PIPE_Q;
-  const int npre = PQ ? (nt < 4 ? nt : 4) : (SC_SLOTS == 4 && nt > 1 ? 2 : 1);
-  for (int i = 0; i < npre; ++i) dm.issue(D, nd, (t0 + i) * SC_COLS, lbase + (uint32_t)i * TI::BYTES);
-  // query fragments by buffer loads: a row past bq reads zero through the resource's range
-  // check instead of a branch, so every wave issues exactly SC_RB * KS loads (the counted
-  // wait in sync(0) relies on it)
-  const __amdgpu_buffer_rsrc_t qrs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(Q), (short)0, (int)(bq * h * 2), 0x00020000);
+  dm.issue(D, nd, t0 * SC_COLS, lbase);
+  if (SC_SLOTS == 4 && nt > 1) dm.issue(D, nd, (t0 + 1) * SC_COLS, lbase + TI::BYTES);
   uint4 qa[SC_RB][KS];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
+  for (int qb = 0; qb < SC_RB; ++qb)
 #pragma unroll
-    for (int qb = 0; qb < SC_RB; ++qb) {
-      const long row = row0 + qb * 16 + (lane & 15);
-      const uint32_t off = row < bq ? (uint32_t)((row * h + ks * 32 + 8 * (lane >> 4)) * 2) : 0x80000000u;
-      qa[qb][ks] = (HN_DIAG & 8) ? make_uint4(lane, ks, qb, 1) : ld16_buf(qrs, off, 0);
-    }
-  if constexpr (!PQ) {
-    // Retire the query loads here, so that hipcc does not place a vmcnt(0) inside the tile
-    // loop (it cannot see the LDS-DMAs and would wait for the tiles in flight every tile).
+    for (int ks = 0; ks < KS; ++ks) qa[qb][ks] = ld_frag(Q, row0 + qb * 16 + (lane & 15), bq, h, ks);
+  // Retire the query loads here, so that hipcc does not place a vmcnt(0) inside the tile
+  // loop (it cannot see the LDS-DMAs and would wait for the tiles in flight every tile).
 #pragma unroll
-    for (int qb = 0; qb < SC_RB; ++qb)
+  for (int qb = 0; qb < SC_RB; ++qb)
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
-        asm volatile("" ::"v"(qa[qb][ks].x), "v"(qa[qb][ks].y), "v"(qa[qb][ks].z), "v"(qa[qb][ks].w));
-  }
+    for (int ks = 0; ks < KS; ++ks)
+      asm volatile("" ::"v"(qa[qb][ks].x), "v"(qa[qb][ks].y), "v"(qa[qb][ks].z), "v"(qa[qb][ks].w));
 
   // Tiles travel in pairs: at every even tile, one wait + barrier retires the pair (t, t+1)
   // for every wave and frees slots (t+2)%4, (t+3)%4 (last read before this barrier), into
@@ -216,25 +164,10 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
   // With two slots (h 512) every tile is retired alone and the next one requested into
   // the slot its predecessor freed.
   auto sync = [&](int t) {
-    if (HN_DIAG & 1) {
-      if (t == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if ((t & 1) == 0) __builtin_amdgcn_s_barrier();
-      return;
-    }
     if (SC_SLOTS == 2) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       if (t + 1 < nt) dm.issue(D, nd, (t0 + t + 1) * SC_COLS, lbase + (uint32_t)((t + 1) % 2) * TI::BYTES);
-    } else if (PQ && t == 0) {
-      // tiles 0 and 1 landed; tiles 2, 3 (issued before the query loads) and the query
-      // loads may still be in flight; tiles 2 and 3 are already requested
-      if constexpr (PQ) {
-        constexpr int QL = (HN_DIAG & 8) ? 0 : SC_RB * KS;
-        static_assert(QL + 2 * TI::DPW <= 63, "vmcnt range");
-        if (npre == 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QL + 2 * TI::DPW) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_s_barrier();
     } else if ((t & 1) == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -244,7 +177,6 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
   };
   // Chunk maxima of tile t (masked form: positive -> -1, documents past nd -> -inf).
   auto chunk_max = [&](const f32x4 (&a)[4][SC_RB], int t, bool masked) {
-    if (HN_DIAG & 4) return;
     const int n0 = (int)((t0 + t) * SC_COLS);
     const bool diag = label_off >= 0 && label_off + row0 < n0 + SC_COLS && n0 < label_off + row0 + SC_RB * 16;
 #pragma unroll
@@ -266,7 +198,10 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
             if (doc >= lim) v[db * 4 + r] = -FLT_MAX;
           }
       }
-      const float m = rowgroup_max4(max16(v));
+      float m = fmaxf(fmaxf(v[0], v[1]), v[2]);
+#pragma unroll
+      for (int j = 3; j < 15; j += 2) m = fmaxf(fmaxf(m, v[j]), v[j + 1]);
+      m = rowgroup_max4(fmaxf(m, v[15]));
       if (lane < 16) cms[t * SC_ROWS + wave * SC_RB * 16 + qb * 16 + lane] = m;
     }
   };
@@ -275,29 +210,18 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
   // the fragment reads of k-step ks+2, the 8 MFMAs of ks, then one slice of the epilogue,
   // so the LDS reads run two k-steps ahead and the epilogue VALU fills MFMA issue gaps
   // (hipcc otherwise sinks every read to just before its MFMA and clusters the VALU).
-  // fragment ring: k-step ks of a tile in fa[(ks + OFF) % 3]. PRE_IN: k-steps 0, 1 were
-  // requested by the previous tile (the first of a pair, both in LDS since the pair's
-  // barrier), PRE_OUT: request the next tile's first two k-steps during the last two.
-  uint4 fa[3][4];
-  auto frag_of = [&](const char* img, int ks, int db) {
-    return *reinterpret_cast<const uint4*>(img + TI::off(db * 16 + (lane & 15), ks * 4 + (lane >> 4)));
-  };
-  auto tile = [&](f32x4 (&acc)[4][SC_RB], const f32x4 (&prev)[4][SC_RB], int t, bool epi, auto pre_in,
-                  auto pre_out) {
-    constexpr int OFF = decltype(pre_in)::value ? KS % 3 : 0;
-    constexpr bool PRE_OUT = decltype(pre_out)::value;
+  auto tile = [&](f32x4 (&acc)[4][SC_RB], const f32x4 (&prev)[4][SC_RB], int t, bool epi) {
     const char* img = lds + (t % SC_SLOTS) * TI::BYTES;
-    const char* nimg = lds + ((t + 1) % SC_SLOTS) * TI::BYTES;
 #pragma unroll
     for (int db = 0; db < 4; ++db)
 #pragma unroll
       for (int qb = 0; qb < SC_RB; ++qb) acc[db][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (!decltype(pre_in)::value) {
+    uint4 fa[3][4];
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int db = 0; db < 4; ++db) fa[(ks + OFF) % 3][db] = frag_of(img, ks, db);
-    }
+      for (int db = 0; db < 4; ++db)
+        fa[ks][db] = *reinterpret_cast<const uint4*>(img + TI::off(db * 16 + (lane & 15), ks * 4 + (lane >> 4)));
     // epilogue slice i: query block i / 3; two half-maxima (documents 0-31, 32-63), then
     // the 4-row-group reduction and the store
     float m = 0.f;
@@ -306,8 +230,9 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
       if (qb >= SC_RB) return;
       if (part < 2) {
         const f32x4 x = prev[2 * part][qb], y = prev[2 * part + 1][qb];
-        const float hm = vmax3(vmax3(x[0], x[1], x[2]), vmax3(x[3], y[0], y[1]), vmax3(y[2], y[3], y[3]));
-        m = part == 0 ? hm : vmax3(m, hm, hm);
+        const float hm =
+            fmaxf(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])), fmaxf(fmaxf(y[0], y[1]), fmaxf(y[2], y[3])));
+        m = part == 0 ? hm : fmaxf(m, hm);
       } else {
         m = rowgroup_max4(m);
         if (lane < 16) cms[(t - 1) * SC_ROWS + wave * SC_RB * 16 + qb * 16 + lane] = m;
@@ -318,26 +243,21 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
     for (int ks = 0; ks < KS; ++ks) {
       if (ks + 2 < KS) {
 #pragma unroll
-        for (int db = 0; db < 4; ++db) fa[(ks + 2 + OFF) % 3][db] = frag_of(img, ks + 2, db);
-      } else if (PRE_OUT) {
-#pragma unroll
-        for (int db = 0; db < 4; ++db) fa[(ks + 2 + OFF) % 3][db] = frag_of(nimg, ks + 2 - KS, db);
+        for (int db = 0; db < 4; ++db)
+          fa[(ks + 2) % 3][db] =
+              *reinterpret_cast<const uint4*>(img + TI::off(db * 16 + (lane & 15), (ks + 2) * 4 + (lane >> 4)));
       }
 #pragma unroll
       for (int db = 0; db < 4; ++db)
 #pragma unroll
-        for (int qb = 0; qb < SC_RB; ++qb) {
-          if (HN_DIAG & 2)
-            asm volatile("" ::"v"(fa[(ks + OFF) % 3][db].x), "v"(qa[qb][ks].x));
-          else
-            acc[db][qb] = ttg::mma<bf16_t>(fa[(ks + OFF) % 3][db], qa[qb][ks], acc[db][qb]);
-        }
-      if (epi && !(HN_DIAG & 4)) {
-        constexpr int NSL = 3 * SC_RB;  // slices spread evenly over the k-steps
-#pragma unroll
-        for (int i = ks * NSL / KS; i < (ks + 1) * NSL / KS; ++i) slice(i);
-      }
+        for (int qb = 0; qb < SC_RB; ++qb)
+          acc[db][qb] = ttg::mma<bf16_t>(fa[ks % 3][db], qa[qb][ks], acc[db][qb]);
+      if (epi) slice(ks);
       __builtin_amdgcn_sched_barrier(0);
+    }
+    if (epi) {
+#pragma unroll
+      for (int i = KS; i < 3 * SC_RB; ++i) slice(i);
     }
   };
   f32x4 accA[4][SC_RB], accB[4][SC_RB];
@@ -347,29 +267,24 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
     return (label_off >= 0 && label_off + row0 < n0 + SC_COLS && n0 < label_off + row0 + SC_RB * 16) ||
            n0 + SC_COLS > nd;
   };
-  // pairs of tiles (4-slot ring): the first of a pair hands the second its first fragments
-  using pre_t = std::bool_constant<SC_SLOTS == 4 && HN_PAIR_PREFETCH>;
-  using no_t = std::false_type;
-  auto step = [&](f32x4 (&cur)[4][SC_RB], const f32x4 (&prev)[4][SC_RB], int t, auto pre_in, auto pre_out) {
+  auto step = [&](f32x4 (&cur)[4][SC_RB], const f32x4 (&prev)[4][SC_RB], int t) {  // t >= 1
     sync(t);
     if (special(t - 1)) {
-      tile(cur, prev, t, false, pre_in, pre_out);
+      tile(cur, prev, t, false);
       chunk_max(prev, t - 1, true);
     } else {
-      tile(cur, prev, t, true, pre_in, pre_out);
+      tile(cur, prev, t, true);
     }
   };
   sync(0);
-  if (nt > 1) tile(accB, accA, 0, false, no_t{}, pre_t{});
-  else tile(accB, accA, 0, false, no_t{}, no_t{});
+  tile(accB, accA, 0, false);
   int t = 1;
   for (; t + 1 < nt; t += 2) {
-    step(accA, accB, t, pre_t{}, no_t{});                 // second of a pair
-    if (t + 2 < nt) step(accB, accA, t + 1, no_t{}, pre_t{});  // first of the next pair
-    else step(accB, accA, t + 1, no_t{}, no_t{});
+    step(accA, accB, t);
+    step(accB, accA, t + 1);
   }
   if (t < nt) {
-    step(accA, accB, t, pre_t{}, no_t{});
+    step(accA, accB, t);
     chunk_max(accA, t, special(t));
   } else {
     chunk_max(accB, t - 1, special(t - 1));
@@ -446,6 +361,10 @@ __global__ __launch_bounds__(RS_THREADS) void hn_rescore_kernel(const bf16_t* __
   }
   __syncthreads();
   // the segment's entries, 4 per 16-byte load (seg * k is a multiple of 4)
+  // The list order depends on the LDS atomic's arbitration, but no output does: each
+  // entry e's 64 scores go to cand[e] and are computed by lanes whose B fragment is that
+  // entry's query row only (an MFMA output element C[doc][query] reads one A row and one
+  // B row), so which wave or which lane group takes the entry changes nothing.
   const int total = (int)(seg1 - seg) * k;
   const int4* s4 = reinterpret_cast<const int4*>(sel + seg * k);
 #pragma unroll 4

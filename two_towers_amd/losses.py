@@ -134,7 +134,7 @@ class _MarginFn(torch.autograd.Function):
         B, h = qn.shape
         dqn = torch.empty_like(qn)
         ddn = torch.zeros_like(dn)
-        ws = torch.empty(_lib.load().tt_margin_bwd_ws_size(B), dtype=torch.uint8, device=qn.device)
+        ws = torch.empty(_lib.load().tt_margin_bwd_ws_size(B, dn.shape[0], h, idx.shape[1]), dtype=torch.uint8, device=qn.device)
         gdev = gout.detach().float().reshape(1).contiguous()  # read by the kernels: no host sync
         call("tt_margin_bwd", qn.data_ptr(), B, dn.data_ptr(), dn.shape[0], h, label_offset, idx.data_ptr(),
              idx.shape[1], margin, gdev.data_ptr(), dqn.data_ptr(), ddn.data_ptr(), ws.data_ptr(),

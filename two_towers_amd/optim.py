@@ -10,7 +10,7 @@ import ctypes
 
 import torch
 
-from . import _lib
+from . import _lib, towers
 from ._lib import call, stream_ptr
 
 _MAXT = 48
@@ -46,6 +46,10 @@ class Adam(torch.optim.Optimizer):
                     raise _lib.TTError("two_towers_amd Adam expects contiguous fp32 parameters and gradients")
                 st["step"] += 1
                 buckets.setdefault(int(st["step"].item()), []).append(p)
+            # the device's step guard: non-zero when a column-split GRU forward since the
+            # last step timed out (towers.watch_gru_status); the kernel then changes nothing
+            dev = ps[0].device
+            guard = towers.step_guard(dev)
             for step, plist in buckets.items():
                 for i in range(0, len(plist), _MAXT):
                     chunk = plist[i:i + _MAXT]
@@ -55,8 +59,11 @@ class Adam(torch.optim.Optimizer):
                     call("tt_adam_multi", arr(chunk), arr([p.grad for p in chunk]),
                          arr([self.state[p]["exp_avg"] for p in chunk]),
                          arr([self.state[p]["exp_avg_sq"] for p in chunk]), sizes, n, group["lr"], b1, b2,
-                         group["eps"], group["weight_decay"], step, stream_ptr(chunk[0].device))
+                         group["eps"], group["weight_decay"], step, guard.data_ptr(), stream_ptr(dev))
             # the kernel writes through raw pointers: record the in-place update for autograd
             # and for the packed-weight cache of the towers (towers._packed)
             torch.autograd.graph.increment_version(ps)
+        for g in {towers.step_guard(p.device) for group in self.param_groups for p in group["params"]
+                  if p.grad is not None}:
+            g.zero_()  # stream-ordered after every launch above
         return loss

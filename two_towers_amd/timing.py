@@ -14,7 +14,7 @@ import torch
 
 enabled = False
 _records = defaultdict(list)
-_kernels = {}
+_kernels = defaultdict(list)  # region -> kernel names it launched, in first-seen order
 
 
 def reset():
@@ -26,12 +26,13 @@ def reset():
 def region(name: str, launches: int, work: float, nbytes: float = 0.0, kernel: str | None = None):
     """work = algorithmic FLOPs (or bytes for pure data movement), nbytes =
     algorithmic HBM bytes of the region (inputs read once + outputs written once),
-    kernel = the name of the kernel the region launches (as rocprofv3 prints it)."""
+    kernel = the name of the kernel the region launches (as rocprofv3 prints it); a region
+    entered with different kernels (the two GRU layers' instances) keeps every name."""
     if not enabled:
         yield
         return
-    if kernel:
-        _kernels[name] = kernel
+    if kernel and kernel not in _kernels[name]:
+        _kernels[name].append(kernel)
     s = torch.cuda.Event(enable_timing=True)
     e = torch.cuda.Event(enable_timing=True)
     s.record()
@@ -51,5 +52,5 @@ def summary():
         b = sum(r[4] for r in recs)
         out[name] = dict(ms_total=ms, launches=n, work=w, bytes=b, ms_per_launch=ms / max(n, 1),
                          work_per_launch=w / max(n, 1), bytes_per_launch=b / max(n, 1), calls=len(recs),
-                         kernel=_kernels.get(name, name))
+                         kernel=" | ".join(_kernels.get(name) or [name]), kernels=list(_kernels.get(name) or []))
     return out

@@ -122,13 +122,30 @@ def _alloc(shape, dt, dev):
 # tt_gru_fwd runs the column-split kernel (member workgroups that exchange h every step)
 # only with a workspace from the caller (include/tt_hip.h tt_gru_fwd_ws_size). Its first
 # word is a status the kernels set when a member wait timed out -- the launch's outputs
-# are then invalid. After each forward the word is copied to pinned host memory on the
-# stream (no device synchronisation); check_gru_status() raises GruTimeoutError for any
-# such launch. TowersFn.forward checks every earlier forward (waiting on its event: the
-# host is at most the GPU's queue ahead, which still holds later work, so the GPU never
-# idles for it), TowersFn.backward the ones already finished.
+# are then invalid. Two things follow from it, neither of which synchronises the host:
+#  * on the device, the word is OR-ed into a per-device step guard; two_towers_amd.Adam
+#    passes the guard to tt_adam_multi, which then leaves every parameter and moment
+#    unchanged, and clears it after the step -- an invalid forward can never update the
+#    weights, whatever the host has not yet seen;
+#  * on the host, the word is copied to pinned memory on the stream; check_gru_status()
+#    raises GruTimeoutError for any such launch. TowersFn.forward checks every earlier
+#    forward (waiting on its event: the host is at most the GPU's queue ahead, which still
+#    holds later work, so the GPU never idles for it), TowersFn.backward the ones already
+#    finished.
 _status_lock = threading.Lock()
 _status_pending: list = []  # (event, pinned int32[1])
+_step_guard: dict = {}  # device -> int32[1]: OR of the status words since the last optimiser step
+
+
+def step_guard(dev) -> torch.Tensor:
+    """The device's step-guard word (int32[1]; non-zero: a forward since the last optimiser
+    step timed out)."""
+    dev = torch.device(dev)
+    with _status_lock:
+        g = _step_guard.get(dev)
+        if g is None:
+            g = _step_guard[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return g
 
 
 def gru_fwd_workspace(nrec, B, T, H, dt, dev):
@@ -145,11 +162,16 @@ def gru_fwd_workspace(nrec, B, T, H, dt, dev):
 
 
 def watch_gru_status(ws):
-    """Queue an asynchronous read-back of ws's status word (after the launches using it)."""
-    host = torch.empty(1, dtype=torch.int32, pin_memory=True)
-    host.copy_(ws[:4].view(torch.int32), non_blocking=True)
-    ev = torch.cuda.Event()
-    ev.record()
+    """After the launches using ws (on its device's current stream): fold its status word
+    into the device's step guard and queue an asynchronous read-back for the host."""
+    with torch.cuda.device(ws.device):
+        st = torch.cuda.current_stream(ws.device)
+        word = ws[:4].view(torch.int32)
+        step_guard(ws.device).bitwise_or_(word)
+        host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        host.copy_(word, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(st)
     with _status_lock:
         _status_pending.append((ev, host))
 
@@ -174,7 +196,8 @@ def check_gru_status(wait: bool = True):
     if bad:
         raise _lib.GruTimeoutError(
             f"{bad} column-split GRU forward launch(es) timed out waiting for a member workgroup "
-            "(not all workgroups were resident); their outputs are invalid. Set option gru_fwd_xc=0 "
+            "(not all workgroups were resident); their outputs are invalid and the optimiser step "
+            "that followed (two_towers_amd.Adam) left the weights unchanged. Set option gru_fwd_xc=0 "
             "(env TT_GRU_FWD_XC=0) to use the row-owning kernel.")
 
 

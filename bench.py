@@ -156,7 +156,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 PMC_SUMMARY = os.path.join(_HERE, "profiles", "r04_pmc_summary.json")
 # the CPU baseline at the metric's own batch (bench.py --cpu-only --cpu-batch 8192 --cpu-steps 2)
 CPU_B8192 = os.path.join(_HERE, "profiles", "r04_cpu_baseline_b8192.json")
-REGION_KERNEL = {"gru_bwd": ("gru_bwd_step<", "gru_bwd_big", "gru_bwd_rows<"), "gru_fwd": ("gru_fwd_xcp<", "gru_fwd_seq<"),
+REGION_KERNEL = {"gru_bwd": ("gru_bwd_step<", "gru_bwd_big", "gru_bwd_rows<"), "gru_fwd": ("gru_fwd_xs<", "gru_fwd_xcp<", "gru_fwd_seq<"),
                  "embed_gather": ("embed_gather_kernel",)}
 
 

@@ -1,0 +1,95 @@
+"""Generate tests/golden/bench_traj.npz: ten training steps of the bench composition run by
+the CPU oracle (oracle/cpu_ref.py), for tests/test_gpu_bench_path.py's trajectory test.
+
+TEST INFRASTRUCTURE ONLY (the oracle takes ~1 minute per step at this size, too long for a
+GPU test, so its trajectory is computed once here and committed as data). Run in the build
+container:
+    PYTHONDONTWRITEBYTECODE=1 python oracle/gen_traj.py
+
+The run (train_enhanced.py:58-63 with the configs[2] loss):
+EnhancedTwoTowerModel(300, 256) initialised by torch.manual_seed(SEED_MODEL) (the model's
+own nn.GRU / nn.Linear defaults, enhanced_two_tower.py:17-48) and rounded to bf16, B 512,
+T 64, two batches of bf16-rounded N(0, 0.25) inputs alternating, dropout 0.1 with the
+per-step, per-tower seeds the GPU model draws from torch.manual_seed(SEED_DROP), get_hard_negatives
+k 5 over the in-batch documents + MarginRankingLoss(0.2) on the mined rows
+(enhanced_two_tower.py:84-133, ties to the lower index), torch.optim.Adam(lr 1e-3) on fp32
+master weights whose forward sees their bf16 rounding (the compute precision of the path
+under test). Stored: the per-step losses and mined indices, and for every parameter 64
+fixed positions of its initial and final values plus the norm of its total change.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from oracle import cpu_ref  # noqa: E402
+
+E, HID, T, B, K, STEPS, LR = 300, 256, 64, 512, 5, 10, 1e-3
+SEED_MODEL, SEED_DATA, SEED_DROP, SEED_POS = 51, 52, 53, 54
+NPOS = 64
+
+
+def bf16(x):
+    return x.to(torch.bfloat16).float()
+
+
+def setup():
+    """Initial weights (bf16-rounded), the two batches and the dropout seeds, exactly as
+    the GPU test builds them."""
+    import two_towers_amd as tta
+    torch.manual_seed(SEED_MODEL)
+    m = tta.EnhancedTwoTowerModel(E, HID)
+    with torch.no_grad():
+        for prm in m.parameters():
+            prm.copy_(bf16(prm))
+    p = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    g = torch.Generator().manual_seed(SEED_DATA)
+    batches = [(bf16(torch.randn(B, T, E, generator=g) * 0.5), bf16(torch.randn(B, T, E, generator=g) * 0.5))
+               for _ in range(2)]
+    torch.manual_seed(SEED_DROP)
+    seeds = [[int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) for _ in range(2)] for _ in range(STEPS)]
+    return p, batches, seeds
+
+
+def positions(p):
+    g = np.random.default_rng(SEED_POS)
+    return {k: g.choice(v.numel(), size=min(NPOS, v.numel()), replace=False).astype(np.int64) for k, v in p.items()}
+
+
+def main():
+    torch.set_num_threads(os.cpu_count() or 8)
+    p, batches, seeds = setup()
+    pos = positions(p)
+    master = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    opt = torch.optim.Adam(list(master.values()), lr=LR)
+    losses, picks = [], []
+    for s in range(STEPS):
+        q, d = batches[s % 2]
+        opt.zero_grad()
+        pb = {k: v + (bf16(v.detach()) - v.detach()) for k, v in master.items()}  # bf16 values, identity grad
+        rq, rd = cpu_ref.forward(q, d, pb, drop_p=0.1, seeds=seeds[s])
+        loss, idx = cpu_ref.hardneg_margin(rq, rd, K, 0.2)
+        loss.backward()
+        opt.step()
+        losses.append(float(loss.detach()))
+        picks.append(idx.numpy().astype(np.int16))
+        print(f"step {s}: loss {losses[-1]:.6f}", flush=True)
+    out = {"losses": np.array(losses), "picks": np.stack(picks), "seeds": np.array(seeds, dtype=np.int64)}
+    for k, v in p.items():
+        out[f"pos/{k}"] = pos[k]
+        out[f"w0/{k}"] = v.reshape(-1)[pos[k]].numpy()
+        out[f"w1/{k}"] = master[k].detach().reshape(-1)[pos[k]].numpy()
+        out[f"dnorm/{k}"] = np.array(float((master[k].detach() - v).norm()))
+    path = os.path.join(ROOT, "tests", "golden", "bench_traj.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path)
+
+
+if __name__ == "__main__":
+    main()

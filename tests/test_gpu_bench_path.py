@@ -274,3 +274,65 @@ def test_reference_size_h512_t128_bf16_matches_oracle():
         assert float((a - b).abs().max() / b.abs().max()) <= 3e-2
     frob, cos, k = _grad_check(dict(m.named_parameters()), p)
     print(f"h 512 T 128: loss {lv:.6f} vs {rv:.6f}; worst gradient {k}: rel {frob:.4f}, cos {cos:.5f}")
+
+
+def test_bench_composition_bf16_adam_trajectory_matches_oracle():
+    """Ten training steps of the bench composition (train_enhanced.py:58-63 with the
+    configs[2] loss): EnhancedTwoTowerModel(300, 256), T 64, B 512, bf16 compute, dropout
+    0.1, HardNegativeMarginLoss (k 5, margin 0.2), two_towers_amd.Adam (lr 1e-3), two
+    batches alternating -- against the oracle's trajectory (tests/golden/bench_traj.npz,
+    oracle/gen_traj.py: cpu_ref forward + mining + margin loss, torch.optim.Adam on fp32
+    master weights whose forward sees their bf16 rounding, the same inputs and the same
+    per-step dropout seeds; ~1 minute of CPU per step, so computed once in the build
+    container). The oracle mines on its own fp32 outputs: a near-tie picked differently
+    moves a row's mean negative cosine by at most ~2e-2 / k, i.e. the loss by ~1e-5.
+    Tolerances: per-step loss within 1e-2 relative (5e-3 at step 0, as the single-step
+    composition test); >= 90 % of the rows pick the oracle's set at every step; for every
+    tensor, at 64 fixed positions, the distance of the final weights from the oracle's at
+    most 0.25 of the distance the oracle's ten steps moved them (Adam's early steps are
+    ~lr * sign(g): an element whose gradient is near zero can move the other way)."""
+    import os
+    gold = np.load(os.path.join(os.path.dirname(__file__), "golden", "bench_traj.npz"))
+    Bq, k, steps, lr = 512, 5, 10, 1e-3
+    m, _ = _model(51)
+    m.train()
+    g = torch.Generator().manual_seed(52)
+    batches = [(_bf16(torch.randn(Bq, T, E, generator=g) * 0.5), _bf16(torch.randn(Bq, T, E, generator=g) * 0.5))
+               for _ in range(2)]
+    w0 = {kk: v.detach().cpu().reshape(-1).clone() for kk, v in m.state_dict().items()}
+    for kk, v in w0.items():  # same initial weights as the oracle's run
+        assert np.array_equal(v[gold[f"pos/{kk}"]].numpy(), gold[f"w0/{kk}"]), kk
+    crit = tta.HardNegativeMarginLoss(k=k, margin=0.2, compute_dtype=torch.bfloat16)
+    opt = tta.Adam(m.parameters(), lr=lr)
+    torch.manual_seed(53)  # the model draws each step's dropout seeds from this stream, as the oracle did
+    gl, agree = [], []
+    for s in range(steps):
+        q, d = batches[s % 2]
+        opt.zero_grad()
+        loss = crit(*m(q.to(DEV), d.to(DEV)))
+        loss.backward()
+        opt.step()
+        gl.append(float(loss.detach()))
+        idx = crit.last_indices.long().cpu().numpy()
+        ridx = gold["picks"][s].astype(np.int64)
+        agree.append(float(np.mean([set(idx[i]) == set(ridx[i]) for i in range(Bq)])))
+    tta.check_gru_status()
+    rl = gold["losses"]
+    for s in range(steps):
+        print(f"step {s}: loss {gl[s]:.6f} vs oracle {rl[s]:.6f} (rel {abs(gl[s] - rl[s]) / abs(rl[s]):.2e}), "
+              f"picks agree {agree[s]:.4f}")
+    assert float(rl.min()) > 0.01, "hinges inactive: the test would compare zeros"
+    for s in range(steps):
+        tol = 5e-3 if s == 0 else 1e-2
+        assert abs(gl[s] - rl[s]) <= tol * abs(rl[s]), (s, gl[s], rl[s])
+        assert agree[s] >= 0.90, (s, agree[s])
+    worst, wk = 0.0, ""
+    for kk, v in m.state_dict().items():
+        pos = gold[f"pos/{kk}"]
+        a = v.detach().cpu().reshape(-1)[pos].double().numpy()
+        b, a0 = gold[f"w1/{kk}"].astype(np.float64), gold[f"w0/{kk}"].astype(np.float64)
+        r = float(np.linalg.norm(a - b) / (np.linalg.norm(b - a0) + 1e-30))
+        if r > worst:
+            worst, wk = r, kk
+    print(f"final weights: worst ||w - w_ref|| / ||w_ref - w0|| = {worst:.3e} ({wk})")
+    assert worst <= 0.25, (wk, worst)

@@ -133,16 +133,17 @@ def _assert_equivalent(outs_p, outs_s, B, T, H, bhn):
     assert not bad, f"persistent vs per-step forward differ: {bad}"
 
 
-@pytest.mark.parametrize("xc", [0, 1])
-def test_bench_grid_persistent_forward_matches_per_step(xc):
+@pytest.mark.parametrize("xc,xs", [(0, 1), (1, 1), (1, 0)])
+def test_bench_grid_persistent_forward_matches_per_step(xc, xs):
     """configs[2] layer-0 shape: B 8192, T 64, H 512, 2 towers x 2 directions in one
     launch, dropout 0.1 on the X1 copy: the persistent forward (xc 1: the column-split
-    gru_fwd_xcp the bench runs; xc 0: the row-owning gru_fwd_seq<4,8>) vs T launches of
+    forward the bench runs, xs 1 its matrix/vector-wave form gru_fwd_xs, xs 0 the
+    single-role gru_fwd_xcp; xc 0: the row-owning gru_fwd_seq<4,8>) vs T launches of
     gru_fwd_step."""
     B, T, H, ntow = 8192, 64, 512, 2
     G, whh, bhn = _inputs(ntow, B, T, H, seed=3)
     outs_s = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=1)
-    with option("gru_fwd_xc", xc):
+    with option("gru_fwd_xc", xc), option("gru_fwd_xs", xs):
         outs_p = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=0)
     assert (outs_p[4] is not None) == (xc == 1)
     _assert_equivalent(outs_p, outs_s, B, T, H, bhn)
@@ -151,7 +152,7 @@ def test_bench_grid_persistent_forward_matches_per_step(xc):
 @pytest.mark.parametrize("H,B,T,ntow", [(512, 1000, 12, 2), (256, 1000, 12, 2), (512, 3000, 5, 2), (512, 70, 3, 2),
                                         (256, 64, 1, 2), (512, 5000, 7, 1), (256, 8192, 4, 2), (512, 300, 2, 1)])
 def test_column_split_forward_matches_per_step(H, B, T, ntow):
-    """gru_fwd_xcp forced (option gru_fwd_xc = 2) wherever it applies: the H/64 member
+    """The column-split forward forced (option gru_fwd_xc = 2) wherever it applies: the H/64 member
     workgroups of a group exchange h every step through the caller's workspace. Rows per
     group that are not a multiple of the 256-row round (B 3000 over 8 groups per
     recurrence: 375 = 256 + 119), groups with no rows at all (B 70, B 64), one tower
@@ -163,11 +164,13 @@ def test_column_split_forward_matches_per_step(H, B, T, ntow):
     # 6: every image store write-through; 18 / 22: a group's members are consecutive blocks,
     # i.e. dealt over the 8 XCDs, so the exchange really crosses XCD L2s (the members see
     # different XCC ids and take the write-through hand-off; 18 checks that they do)
-    for mode in (2, 6, 18, 22):
-        with option("gru_fwd_xc", mode):
-            outs_p = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=0)
-        assert outs_p[0] == 1 and outs_p[4] is not None, mode
-        _assert_equivalent(outs_p, outs_s, B, T, H, bhn)
+    # H 512 runs both forms: gru_fwd_xs (matrix / vector waves, the default) and gru_fwd_xcp
+    for xs in ((1, 0) if H == 512 else (1,)):
+        for mode in (2, 6, 18, 22):
+            with option("gru_fwd_xc", mode), option("gru_fwd_xs", xs):
+                outs_p = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=0)
+            assert outs_p[0] == 1 and outs_p[4] is not None, (xs, mode)
+            _assert_equivalent(outs_p, outs_s, B, T, H, bhn)
 
 
 def test_column_split_forward_without_workspace_runs_row_owning_kernel():
@@ -223,8 +226,17 @@ def test_column_split_member_timeout_is_reported_and_not_sticky():
     moments = {id(p): (opt.state[p]["exp_avg"].clone(), opt.state[p]["exp_avg_sq"].clone()) for p in m.parameters()}
     with option("gru_xc_spins", 14), option("gru_xc_skip", 1):
         vq, vd = m(q, q)
-    crit(vq, vd).backward()
-    opt.step()
+    # the host-side check of TowersFn.backward (wait=False) would raise already when the
+    # forward has finished; switched off here so the step runs as it does when the host is
+    # still ahead of the GPU -- the case only the device-side guard covers
+    from two_towers_amd import towers
+    host_check = towers.check_gru_status
+    towers.check_gru_status = lambda wait=True: None
+    try:
+        crit(vq, vd).backward()
+        opt.step()
+    finally:
+        towers.check_gru_status = host_check
     torch.cuda.synchronize()
     for k, v in m.state_dict().items():
         assert torch.equal(v, before[k]), k

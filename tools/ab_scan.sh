@@ -1,5 +1,7 @@
 #!/bin/bash
-# hn_scan A/B: rocprofv3 kernel stats over tools/bench_score.py hardneg for each library.
+# hn_scan A/B: rocprofv3 kernel traces over tools/bench_score.py hardneg for each library,
+# summarised per (library run, kernel, grid) as the median traced dispatch duration (the two
+# shapes launch the same kernels, so the stats file alone would average them together).
 # Usage: tools/ab_scan.sh TAG [lib.so ...]   (default: libtt_hip.so libtt_hip_exp.so)
 set -o pipefail
 TAG=${1:-x}; shift
@@ -14,10 +16,15 @@ for rep in 1 2; do for lib in $LIBS; do
     --hn-shapes 8192x8192x256,8192x65536x256 > $OUT/${lib%.so}_$rep.log 2>&1 || { echo "prof $lib $rep failed"; exit 1; }
 done; done
 python - $OUT <<'PY'
-import csv, glob, sys
+import collections, csv, glob, sys
 for d in sorted(glob.glob(sys.argv[1] + "/libtt*/")):
-    f = glob.glob(d + "**/*kernel_stats.csv", recursive=True)[0]
+    f = glob.glob(d + "**/*kernel_trace.csv", recursive=True)[0]
+    agg = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
-        if "hn_" in r["Name"]:
-            print(d.rstrip("/").split("/")[-1], r["Name"].split("(")[0][-28:], r["Calls"], round(float(r["AverageNs"]) / 1e3, 2))
+        if "hn_" in r["Kernel_Name"]:
+            name = r["Kernel_Name"].split("(")[0].split("::")[-1]
+            agg[(name, r["Grid_Size_X"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    for (name, grid), v in sorted(agg.items()):
+        v.sort()
+        print(d.rstrip("/").split("/")[-1], name, "grid", grid, len(v), "median us", round(v[len(v) // 2], 2))
 PY

@@ -41,6 +41,7 @@ enum Opt {
   OPT_GEMM_BUF,         // 0: 256x256 GEMM operand DMAs through per-lane pointers instead of buffer resources
   OPT_GEMM_ORDER,       // 1: persistent GEMM tiles in column groups per XCD
   OPT_GRU_STEP_RING,    // LDS stages of the per-step GRU kernels' product (2: double buffer; fwd uses <= 3)
+  OPT_GRU_FWD_XS,       // 1: column-split forward with matrix and vector waves (gru_fwd_xs, H 512); 0: gru_fwd_xcp
   OPT_N
 };
 int opt(Opt o);

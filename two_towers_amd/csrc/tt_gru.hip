@@ -1732,6 +1732,262 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
   }
 }
 
+// gru_fwd_xs: the column-split forward with the two kinds of work on different waves.
+// gru_fwd_xcp gives each SIMD ONE wave that issues both the chunk MFMAs (96 per 32-row
+// chunk) and the gate arithmetic, stores and exchange traffic (~375 vector instructions
+// per chunk): in-order issue exposes every dependency stall, ~4k cycles per chunk
+// against ~2.5k of issue. Here 8 waves share the CU, two per SIMD:
+//   matrix waves 0-3 hold the member's W_hh rows in their accumulator registers (as
+//     gru_fwd_xcp's waves) and compute the gates of chunk i + 1 (h from the LDS slot,
+//     result staged in gate buffer (i + 1) & 1);
+//   vector waves 4-7 finish chunk i: gates from buffer i & 1, the fp32 state of the round
+//     in their own registers (no LDS), gru_cell, the exchange and output stores, the G
+//     prefetch, the h chunk two ahead into the slot chunk i's MFMAs used, the half-step
+//     counters;
+// so each SIMD's matrix pipe and vector issue are fed by different waves (MI355X_MICROARCH.md
+// "Two waves per SIMD"), with ONE barrier per chunk. The MFMA sequence per chunk and the
+// cell are gru_fwd_xcp's (same k order from zero, gru_cell): bit-identical outputs.
+namespace xs {
+constexpr int NT = 512;
+template <int H>
+struct Cfg {
+  static constexpr int SLOT = xc::Cfg<H>::SLOT;
+  static constexpr int LDS = 2 * SLOT + 2 * xc::STG;
+};
+static_assert(Cfg<512>::LDS <= 163840, "gru_fwd_xs LDS budget");
+}  // namespace xs
+
+template <int H, bool DROP>
+__global__ __launch_bounds__(xs::NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void gru_fwd_xs(FwdArgs a, XcWs ws) {
+  using C = xc::Cfg<H>;
+  constexpr int M = C::M, NKT = C::NKT, QPW = C::QPW;
+  __shared__ __attribute__((aligned(16))) char lds[xs::Cfg<H>::LDS];
+  char* slots = lds;
+  float* stgb = reinterpret_cast<float*>(lds + 2 * C::SLOT);  // [2][32 rows][192] fp32
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const bool mw = wave < 4;                 // matrix wave
+  const int vw = wave - 4, vt = tid - 256;  // vector wave / thread index
+  const int xcd = blockIdx.x & 7, jj = blockIdx.x >> 3;
+  const int grp = ws.xmap ? (int)blockIdx.x / M : xcd * ws.qg + jj / M;
+  const int mem = ws.xmap ? (int)blockIdx.x % M : jj % M;
+  const int rz = grp % ws.nrec, gi = grp / ws.nrec;
+  const FwdRec R = a.r[rz];
+  const int T_ = a.T, B = a.B;
+  const int gb0 = gi * ws.rpg;
+  xc_gu32* cw = (xc_gu32*)(uintptr_t)(ws.cnt + grp * xc::CSTR);
+  xc_gu32* cntA = cw;
+  xc_gu32* cntB = cw + 2;
+  const bool publish = !(grp == 0 && mem == ws.skip - 1);
+  bf16_t* xbg = ws.xb + (long)grp * 2 * xc::RR * H;
+  const __amdgpu_buffer_rsrc_t rx[2] = {tt_rsrc(xbg), tt_rsrc(xbg + xc::RR * H)};
+  const bool fast = xc_group_on_one_xcd(ws.cnt + grp * xc::CSTR, M, mem, ws.fast_ok != 0, ws);
+  if (ws.skew > 0 && (grp & 1))
+    for (int i = 0; i < ws.skew; ++i) __builtin_amdgcn_s_sleep(127);
+  const int NS = ws.nround * T_;
+  struct Step {
+    int s, t, rb0, nrow;
+  };
+  auto step_of = [&](int idx) {
+    Step q;
+    const int r = idx / T_;
+    q.s = idx - r * T_;
+    q.t = R.dir ? T_ - 1 - q.s : q.s;
+    q.rb0 = gb0 + r * xc::RR;
+    q.nrow = min(min(ws.rpg - r * xc::RR, xc::RR), B - q.rb0);
+    return q;
+  };
+  // zero h for step 0's chunks 0 and 1 (every wave helps), then the roles split
+  for (int i = tid; i < 2 * C::SLOT / 16; i += xs::NT) reinterpret_cast<float4*>(slots)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  if (mw) {
+    // ---------------------------------------------------------------- matrix waves
+    tt_u32x4 wa[3][NKT];
+    {
+      const bf16_t* W = static_cast<const bf16_t*>(R.whh);
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+          wa[g][kt] = *reinterpret_cast<const tt_u32x4*>(
+              W + (long)(g * H + 64 * mem + 16 * wave + (lane & 15)) * H + kt * 32 + (lane >> 4) * 8);
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt) asm volatile("" : "+v"(wa[g][kt]));
+    }
+    // gates of one chunk from h slot `sl` into gate buffer `gb` (C^T: 4 units of a row per lane)
+    auto chunk = [&](const char* sl, float* gb) {
+      f32x4 acc[2][3];
+      const char* base = sl + lane * 16;
+      auto frag = [&](int kt, int rb) { return *reinterpret_cast<const tt_u32x4*>(base + (kt * 2 + rb) * 1024); };
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int g = 0; g < 3; ++g) acc[rb][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      tt_u32x4 f[3][2];
+      f[0][0] = frag(0, 0); f[0][1] = frag(0, 1);
+      f[1][0] = frag(1, 0); f[1][1] = frag(1, 1);
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        if (kt + 2 < NKT) {
+          f[(kt + 2) % 3][0] = frag(kt + 2, 0);
+          f[(kt + 2) % 3][1] = frag(kt + 2, 1);
+        }
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+          for (int g = 0; g < 3; ++g)
+            acc[rb][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8v, wa[g][kt]), __builtin_bit_cast(bf16x8v, f[kt % 3][rb]), acc[rb][g], 0, 0, 0);
+      }
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int g = 0; g < 3; ++g)
+          *reinterpret_cast<f32x4*>(gb + stg_off(rb * 16 + (lane & 15), g * 64 + 16 * wave + 4 * (lane >> 4))) = acc[rb][g];
+    };
+    chunk(slots, stgb);  // step 0, chunk 0 (zero h)
+    __syncthreads();
+    for (int idx = 0; idx < NS; ++idx) {
+      const bool has_next = idx + 1 < NS;
+#pragma unroll
+      for (int c = 0; c < xc::NCH; ++c) {
+        if (c + 1 < xc::NCH || has_next) chunk(slots + ((c + 1) & 1) * C::SLOT, stgb + ((c + 1) & 1) * (xc::STG / 4));
+        __syncthreads();
+      }
+    }
+    return;
+  }
+  // ------------------------------------------------------------------ vector waves
+  uint32_t ho[QPW];
+#pragma unroll
+  for (int p = 0; p < QPW; ++p) {
+    const int q = vw * QPW + p, kt = q >> 1, rb = q & 1;
+    ho[p] = (uint32_t)(((rb * 16 + (lane & 15)) * H + kt * 32 + (lane >> 4) * 8) * 2);
+  }
+  const int cr = vt >> 3, u0 = (vt & 7) * 8, j = 64 * mem + u0;
+  float bn[8];
+  {
+    const float4 b0 = *reinterpret_cast<const float4*>(R.bhn + j);
+    const float4 b1 = *reinterpret_cast<const float4*>(R.bhn + j + 4);
+    bn[0] = b0.x; bn[1] = b0.y; bn[2] = b0.z; bn[3] = b0.w;
+    bn[4] = b1.x; bn[5] = b1.y; bn[6] = b1.z; bn[7] = b1.w;
+  }
+  const bf16_t* G = static_cast<const bf16_t*>(R.g);
+  bf16_t* Yw = static_cast<bf16_t*>(R.y);
+  bf16_t* X1 = static_cast<bf16_t*>(R.x1);
+  bf16_t* S = static_cast<bf16_t*>(R.save);
+  auto g_rsrc = [&](const Step& q) { return tt_rsrc_n(G + (long)(q.nrow > 0 ? q.rb0 : 0) * T_ * a.ldg, q.nrow > 0); };
+  auto load_g = [&](const Step& q, __amdgpu_buffer_rsrc_t rG, int c, tt_u32x4 (&gx)[3]) {
+    const uint32_t og = c * xc::CR + cr < q.nrow ? (uint32_t)(((c * xc::CR + cr) * T_ + q.t) * (int)a.ldg + j) * 2u
+                                                  : xc::OOB;
+#pragma unroll
+    for (int g = 0; g < 3; ++g) gx[g] = __builtin_amdgcn_raw_buffer_load_b128(rG, (int)og, g * H * 2, XC_G_AUX);
+  };
+  tt_u32x4 hv[QPW];
+  auto load_h = [&](const Step& q, int qidx, int c) {
+    if (q.s == 0) {
+#pragma unroll
+      for (int p = 0; p < QPW; ++p) hv[p] = tt_u32x4{0u, 0u, 0u, 0u};
+    } else {
+#pragma unroll
+      for (int p = 0; p < QPW; ++p)
+        hv[p] = __builtin_amdgcn_raw_buffer_load_b128(rx[(qidx - 1) & 1], (int)ho[p], c * xc::CR * H * 2, 16);
+    }
+  };
+  float st[xc::NCH][8];  // fp32 state of this thread's (row, 8 units) in each chunk of the round
+  Step cur = step_of(0);
+  __amdgpu_buffer_rsrc_t rGc = g_rsrc(cur);
+  tt_u32x4 gq[2][3];
+  load_g(cur, rGc, 0, gq[0]);
+#pragma unroll
+  for (int p = 0; p < QPW; ++p) hv[p] = tt_u32x4{0u, 0u, 0u, 0u};  // step 0, chunk 2
+  __syncthreads();  // the matrix waves' chunk 0
+  for (int idx = 0; idx < NS; ++idx) {
+    const bool has_next = idx + 1 < NS;
+    const Step nxt = step_of(has_next ? idx + 1 : idx);
+    const __amdgpu_buffer_rsrc_t rGn = g_rsrc(nxt);
+    const long r0w = (long)(cur.nrow > 0 ? cur.rb0 : 0) * T_;
+    const bool on = cur.nrow > 0;
+    const __amdgpu_buffer_rsrc_t rY = tt_rsrc_n(Yw + r0w * a.ldy, on);
+    const __amdgpu_buffer_rsrc_t rX1 = tt_rsrc_n(X1 ? X1 + r0w * a.ldy : Yw, on && X1 != nullptr);
+    const __amdgpu_buffer_rsrc_t rS = tt_rsrc_n(S + r0w * 4L * H, on);
+    const __amdgpu_buffer_rsrc_t rdst_h = rx[idx & 1];
+    const int t = cur.t;
+    const bool first = cur.s == 0;
+#pragma unroll
+    for (int c = 0; c < xc::NCH; ++c) {
+      if (c + 1 < xc::NCH) load_g(cur, rGc, c + 1, gq[(c + 1) & 1]);
+      else if (has_next) load_g(nxt, rGn, 0, gq[0]);
+      {
+        const int rr = c * xc::CR + cr;
+        const bool ok = rr < cur.nrow;
+        const float* gb = stgb + (c & 1) * (xc::STG / 4);
+        float xr[8], xz[8], xn[8], lr[8], lz[8], ln[8], y[8], sr[8], sz[8], sn[8], sg[8];
+        const tt_u32x4(&gcur)[3] = gq[c & 1];
+        unpack8(make_uint4(gcur[0][0], gcur[0][1], gcur[0][2], gcur[0][3]), xr);
+        unpack8(make_uint4(gcur[1][0], gcur[1][1], gcur[1][2], gcur[1][3]), xz);
+        unpack8(make_uint4(gcur[2][0], gcur[2][1], gcur[2][2], gcur[2][3]), xn);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float4 v0 = *reinterpret_cast<const float4*>(gb + stg_off(cr, 0 * 64 + u0 + 4 * h));
+          const float4 v1 = *reinterpret_cast<const float4*>(gb + stg_off(cr, 1 * 64 + u0 + 4 * h));
+          const float4 v2 = *reinterpret_cast<const float4*>(gb + stg_off(cr, 2 * 64 + u0 + 4 * h));
+          lr[4 * h] = v0.x; lr[4 * h + 1] = v0.y; lr[4 * h + 2] = v0.z; lr[4 * h + 3] = v0.w;
+          lz[4 * h] = v1.x; lz[4 * h + 1] = v1.y; lz[4 * h + 2] = v1.z; lz[4 * h + 3] = v1.w;
+          ln[4 * h] = v2.x; ln[4 * h + 1] = v2.y; ln[4 * h + 2] = v2.z; ln[4 * h + 3] = v2.w;
+        }
+        const uint32_t grow = (uint32_t)(cur.rb0 + rr) * (uint32_t)T_ + (uint32_t)t;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float hp = first ? 0.f : st[c][e];
+          gru_cell(xr[e], xz[e], xn[e], lr[e], lz[e], ln[e], bn[e], hp, y[e], sr[e], sz[e], sn[e], sg[e]);
+          st[c][e] = y[e];
+        }
+        const uint4 yb = pack8bf(y);
+        if (fast) st16_buf(rdst_h, (uint32_t)(rr * H + j) * 2u, 0, yb);
+        else st16_buf_sc1(rdst_h, (uint32_t)(rr * H + j) * 2u, 0, yb);
+        asm volatile("" ::: "memory");  // exactly 6 stores follow (the publish below waits for the rest)
+        const int lrow = rr * T_ + t;
+        const uint32_t oy = ok ? (uint32_t)(lrow * (int)a.ldy + j) * 2u : xc::OOB;
+        const uint32_t os = ok ? (uint32_t)(lrow * 4 * H + j) * 2u : xc::OOB;
+        st16_buf_aux<XC_OUT_AUX>(rY, (int)oy, yb);
+        st16_buf_aux<XC_OUT_AUX>(rS, (int)os, pack8bf(sr));
+        st16_buf_aux<XC_OUT_AUX>(rS, (int)(os + 2u * H), pack8bf(sz));
+        st16_buf_aux<XC_OUT_AUX>(rS, (int)(os + 4u * H), pack8bf(sn));
+        st16_buf_aux<XC_OUT_AUX>(rS, (int)(os + 6u * H), pack8bf(sg));
+        if constexpr (DROP) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            y[e] *= tt_dropout_scale(R.seed, R.row0 + grow, (uint32_t)(R.col0 + j + e), a.drop_thresh, a.inv_keep);
+          st16_buf_aux<XC_OUT_AUX>(rX1, (int)oy, pack8bf(y));
+        } else {
+          st16_buf_aux<XC_OUT_AUX>(rX1, (int)oy, yb);
+        }
+      }
+      if (c == 3 || c == 7) asm volatile("s_nop 0\n\ts_waitcnt vmcnt(6)" ::: "memory");  // s_nop 0: marker (test_host)
+      // h chunk two ahead into the slot chunk c's MFMAs used (read before the last barrier);
+      // request the one three ahead
+      if (c + 2 < xc::NCH || has_next) {
+#pragma unroll
+        for (int p = 0; p < QPW; ++p)
+          *reinterpret_cast<tt_u32x4*>(slots + (c & 1) * C::SLOT + (vw * QPW + p) * 1024 + lane * 16) = hv[p];
+      }
+      if (c + 3 < xc::NCH) load_h(cur, idx, c + 3);
+      else if (has_next) load_h(nxt, idx + 1, c + 3 - xc::NCH);
+      if (vt == 0) {
+        if (c == 0 && idx > 0) xc_wait(cntB, (unsigned)(M * idx), ws);
+        if (c == 4 && has_next) xc_wait(cntA, (unsigned)(M * (idx + 1)), ws);
+      }
+      __syncthreads();
+      if (vt == 0 && c == 3 && publish) __hip_atomic_fetch_add(cntA, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (vt == 0 && c == 7 && publish) __hip_atomic_fetch_add(cntB, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    cur = nxt;
+    rGc = rGn;
+  }
+}
+
 #ifdef TT_DIAG
 }  // namespace
 extern "C" int tt_diag_fwd_prof(unsigned long long* out) {  // [2048][8] host buffer
@@ -1831,6 +2087,7 @@ struct XcGeo {
 struct XcDev {
   int cus = 0;
   int occ[2][2] = {{0, 0}, {0, 0}};  // [H 256 / 512][DROP]
+  int occ_xs[2] = {0, 0};            // gru_fwd_xs<512, DROP>
 };
 static std::mutex g_xc_mu;
 static XcDev g_xc[64];
@@ -1839,6 +2096,12 @@ template <int H, bool DROP>
 static const void* xc_kernel() {
   return reinterpret_cast<const void*>(&gru_fwd_xcp<H, DROP>);
 }
+template <bool DROP>
+static const void* xs_kernel() {
+  return reinterpret_cast<const void*>(&gru_fwd_xs<512, DROP>);
+}
+// the specialized-wave form (gru_fwd_xs) where it is selected and built (H 512)
+static bool xs_on(int H) { return H == 512 && tt::opt(tt::OPT_GRU_FWD_XS) != 0; }
 
 static int xc_device(XcDev** out) {
   int dev = 0;
@@ -1853,6 +2116,8 @@ static int xc_device(XcDev** out) {
                            {xc_kernel<512, false>(), xc_kernel<512, true>()}};
     for (int h = 0; h < 2; ++h)
       for (int d = 0; d < 2; ++d) TT_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&x.occ[h][d], k[h][d], xc::NT, 0));
+    const void* kx[2] = {xs_kernel<false>(), xs_kernel<true>()};
+    for (int d = 0; d < 2; ++d) TT_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&x.occ_xs[d], kx[d], xs::NT, 0));
     x.cus = cus;
   }
   *out = &x;
@@ -1869,7 +2134,8 @@ static bool xc_geometry(const XcDev& dev, int dtype, int H, int nrec, int B, int
   const int ng = 8 * qg;
   if (qg < 1 || ng > XC_MAX_GROUPS || ng % nrec != 0) return false;
   // every member must be resident at once: one workgroup per CU, grid <= CUs
-  if (dev.occ[H == 512][drop] < 1 || ng * M > dev.cus * dev.occ[H == 512][drop]) return false;
+  const int occ = xs_on(H) ? dev.occ_xs[drop] : dev.occ[H == 512][drop];
+  if (occ < 1 || ng * M > dev.cus * occ) return false;
   const int gpr = ng / nrec;
   // auto mode: only where every group gets at least half a round of rows
   if ((v & 3) == 1 && (long)B < (long)gpr * (xc::RR / 2)) return false;
@@ -1934,8 +2200,11 @@ static int gru_fwd_xc_launch(const FwdArgs& a, int nrec, int B, int T, int H, lo
   FwdArgs ak = a;
   XcWs wk = g.w;
   void* args[] = {&ak, &wk};
-  const void* fn = H == 512 ? (drop ? xc_kernel<512, true>() : xc_kernel<512, false>())
+  const bool xs = xs_on(H);
+  const void* fn = xs ? (drop ? xs_kernel<true>() : xs_kernel<false>())
+                 : H == 512 ? (drop ? xc_kernel<512, true>() : xc_kernel<512, false>())
                             : (drop ? xc_kernel<256, true>() : xc_kernel<256, false>());
+  const int nt = xs ? xs::NT : xc::NT;
   // A plain launch by default: xc_plan has already checked the grid (<= one workgroup per
   // CU) against the occupancy query, which is all a cooperative launch checks on gfx950
   // (MI355X_MICROARCH.md "coop-launch": same residency, +15-19 us per launch), and the
@@ -1944,8 +2213,8 @@ static int gru_fwd_xc_launch(const FwdArgs& a, int nrec, int B, int T, int H, lo
   // profiled process fault in teardown after the profiler's finalisation
   // (profiles/r04_rocprof_crash_k.txt), the plain one does not.
   const hipError_t e = tt::opt(tt::OPT_GRU_XC_COOP)
-                           ? hipLaunchCooperativeKernel(fn, dim3(g.grid), dim3(xc::NT), args, 0, st)
-                           : hipLaunchKernel(fn, dim3(g.grid), dim3(xc::NT), args, 0, st);
+                           ? hipLaunchCooperativeKernel(fn, dim3(g.grid), dim3(nt), args, 0, st)
+                           : hipLaunchKernel(fn, dim3(g.grid), dim3(nt), args, 0, st);
   if (e == hipErrorCooperativeLaunchTooLarge) {
     (void)hipGetLastError();  // clear it: the row-owning kernel runs instead
     return 0;

@@ -29,6 +29,9 @@
 
 namespace {
 
+#ifndef HN_SPREAD  // 0: a tile's due DMAs in one burst at its first k-step (the round-3 form)
+#define HN_SPREAD 1
+#endif
 constexpr int SC_COLS = 64;     // document columns per tile (= per chunk)
 constexpr int SC_RB = 2;        // 16-query MFMA blocks per wave
 constexpr int SC_TPS_MAX = 32;  // tiles per workgroup (chunk-max staging)
@@ -81,14 +84,15 @@ struct ScanDma {
       eoff[i] = n * (32 * KS) + c * 8;
     }
   }
-  TT_DEV void issue(const bf16_t* __restrict__ D, long nd, long n0, uint32_t base) const {
+  // piece i of the tile starting at document n0 into the slot at LDS address base
+  TT_DEV void piece(const bf16_t* __restrict__ D, long nd, long n0, uint32_t base, int i) const {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bf16_t* tb = D + n0 * (32 * KS);
+    const void* src = n0 + doc[i] < nd ? static_cast<const void*>(D + n0 * (32 * KS) + eoff[i]) : ttg::g_tt_zero_page;
+    ttg::dma16(src, __builtin_amdgcn_readfirstlane(base + (uint32_t)(wave * TI::DPW + i) * 1024u));
+  }
+  TT_DEV void issue(const bf16_t* __restrict__ D, long nd, long n0, uint32_t base) const {
 #pragma unroll
-    for (int i = 0; i < TI::DPW; ++i) {
-      const void* src = n0 + doc[i] < nd ? static_cast<const void*>(tb + eoff[i]) : ttg::g_tt_zero_page;
-      ttg::dma16(src, __builtin_amdgcn_readfirstlane(base + (uint32_t)(wave * TI::DPW + i) * 1024u));
-    }
+    for (int i = 0; i < TI::DPW; ++i) piece(D, nd, n0, base, i);
   }
 };
 
@@ -163,16 +167,32 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
   // which the next pair is requested; it lands while this pair is computed.
   // With two slots (h 512) every tile is retired alone and the next one requested into
   // the slot its predecessor freed.
+  // The DMAs of the tiles that become due at tile t's barrier (t + 1 with two slots; t + 2
+  // and t + 3 at the start of a pair) are spread over tile t's k-steps, NPK per k-step,
+  // instead of issued in one burst after the barrier: every wave of the CU reaches that
+  // barrier together, so a burst (8 pieces per wave at h 256, ~100 cycles of issue each)
+  // left the matrix pipes idle. They still all land before the next wait retires them.
+  constexpr int NPD = SC_SLOTS == 2 ? TI::DPW : 2 * TI::DPW;  // pieces due per DMA tile
+  constexpr int NPK = HN_SPREAD ? (NPD + KS - 1) / KS : NPD;  // pieces per k-step (0: all at k-step 0)
   auto sync = [&](int t) {
-    if (SC_SLOTS == 2) {
+    if (SC_SLOTS == 2 || (t & 1) == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (t + 1 < nt) dm.issue(D, nd, (t0 + t + 1) * SC_COLS, lbase + (uint32_t)((t + 1) % 2) * TI::BYTES);
-    } else if ((t & 1) == 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (t + 2 < nt) dm.issue(D, nd, (t0 + t + 2) * SC_COLS, lbase + (uint32_t)((t + 2) % SC_SLOTS) * TI::BYTES);
-      if (t + 3 < nt) dm.issue(D, nd, (t0 + t + 3) * SC_COLS, lbase + (uint32_t)((t + 3) % SC_SLOTS) * TI::BYTES);
+    }
+  };
+  // issue the share of k-step ks of the pieces due at tile t (a tile with no pieces due:
+  // the second of a pair)
+  auto dma_k = [&](int t, int ks) {
+#pragma unroll
+    for (int u = 0; u < NPK; ++u) {
+      const int i = ks * NPK + u;
+      if (i >= NPD) break;
+      if (SC_SLOTS == 2) {
+        if (t + 1 < nt) dm.piece(D, nd, (t0 + t + 1) * SC_COLS, lbase + (uint32_t)((t + 1) % 2) * TI::BYTES, i);
+      } else if ((t & 1) == 0) {
+        const int tt = t + 2 + i / TI::DPW;
+        if (tt < nt) dm.piece(D, nd, (t0 + tt) * SC_COLS, lbase + (uint32_t)(tt % SC_SLOTS) * TI::BYTES, i % TI::DPW);
+      }
     }
   };
   // Chunk maxima of tile t (masked form: positive -> -1, documents past nd -> -inf).
@@ -241,6 +261,7 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
+      dma_k(t, ks);
       if (ks + 2 < KS) {
 #pragma unroll
         for (int db = 0; db < 4; ++db)

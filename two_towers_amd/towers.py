@@ -267,7 +267,8 @@ def _gru_layer_fwd(cfg, xs, K, ldx, packs, layer, B, T, seeds, want_x1, ws):
         else _lib.load().tt_gru_fwd_launches(dtype_code(dt), T, H)
     per = esz * (8 + (1 if want_x1 else 0)) + (0 if nl == 1 else esz + 8)
     if nl == 1 and ws is not None:
-        kname = f"gru_fwd_xcp<{H}, {'true' if want_x1 and cfg.drop_p > 0 else 'false'}>"
+        form = "gru_fwd_xs" if H == 512 and _lib.get_option("gru_fwd_xs") else "gru_fwd_xcp"
+        kname = f"{form}<{H}, {'true' if want_x1 and cfg.drop_p > 0 else 'false'}>"
     elif nl == 1:
         kname = "gru_fwd_seq<"
     else:

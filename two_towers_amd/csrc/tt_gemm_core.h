@@ -26,6 +26,10 @@ typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
+#ifndef TT_SHIFT_BUF  // 0: the time-shifted operand keeps per-piece pointer DMAs (the round-4 form)
+#define TT_SHIFT_BUF 1
+#endif
+
 namespace ttg {
 
 constexpr int KTB = 128;  // K-tile bytes per row
@@ -763,8 +767,8 @@ struct Loop8 {
     }
   };
   template <bool KO, class L>
-  using Half = std::conditional_t<BUF && !L::KSPLIT, std::conditional_t<L::SHIFTED, SHalf<KO, L>, BHalf<KO, L>>,
-                                  PHalf<KO, L>>;
+  using Half = std::conditional_t<BUF && !L::KSPLIT && (!L::SHIFTED || TT_SHIFT_BUF),
+                                  std::conditional_t<L::SHIFTED, SHalf<KO, L>, BHalf<KO, L>>, PHalf<KO, L>>;
 
   TT_DEV static void quad(int mi, int ni, const uint4 (&fa)[2][4], const uint4 (&fb)[2][4], f32x4 (&acc)[TM][TN]) {
     __builtin_amdgcn_s_barrier();

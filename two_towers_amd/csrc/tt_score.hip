@@ -32,18 +32,30 @@ namespace {
 #ifndef HN_SPREAD  // 0: a tile's due DMAs in one burst at its first k-step (the round-3 form)
 #define HN_SPREAD 1
 #endif
+#ifndef HN_DSPLIT  // h 256: 1 = every wave takes all 64 documents of a tile for 32 queries
+#define HN_DSPLIT 2  // (the round-3 form); 2 = half the documents for 64 queries
+#endif
 constexpr int SC_COLS = 64;     // document columns per tile (= per chunk)
-constexpr int SC_RB = 2;        // 16-query MFMA blocks per wave
 constexpr int SC_TPS_MAX = 32;  // tiles per workgroup (chunk-max staging)
 
 // Per width (h = 32 KS). h <= 256: 8 waves (two per SIMD, 256 query rows per workgroup)
 // and a 4-slot LDS tile ring that travels in pairs. h 512: a tile is 64 KiB and the
 // query fragments alone are 128 registers per lane, so 4 waves (one per SIMD, 512
 // registers each, 128 query rows) and a 2-slot ring, one tile per barrier.
+// DH (h 256): the waves split each tile's documents DH ways; a wave then holds RB = 2 DH
+// query blocks (64 queries at DH 2, 128 registers of fragments) and reads only its 32
+// documents' fragments, so every LDS fragment read feeds 4 MFMAs and the workgroup reads
+// each tile from LDS 4 times instead of 8 -- the LDS reads, not the MFMAs, were the
+// largest part of the scan (profiles/r04_hn_scan_diag.txt: 11 of 38 us). The two
+// halves' chunk maxima meet in LDS (ds_max_f32; max is exact in any order).
 template <int KS>
 struct ScanCfg {
   static constexpr int WAVES = KS <= 8 ? 8 : 4;
-  static constexpr int ROWS = WAVES * SC_RB * 16;
+  static constexpr int DH = KS == 8 ? HN_DSPLIT : 1;  // document splits per tile
+  static constexpr int RB = 2 * DH;                   // 16-query MFMA blocks per wave
+  static constexpr int NDB = 4 / DH;                  // 16-document blocks per wave
+  static constexpr int QW = WAVES / DH;               // query groups
+  static constexpr int ROWS = QW * RB * 16;
   static constexpr int SLOTS = KS <= 8 ? 4 : 2;
 };
 
@@ -117,6 +129,7 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
                                                                  float* __restrict__ CM, int map) {
   using TI = ScanTile<KS>;
   constexpr int SC_WAVES = ScanCfg<KS>::WAVES, SC_ROWS = ScanCfg<KS>::ROWS, SC_SLOTS = ScanCfg<KS>::SLOTS;
+  constexpr int SC_RB = ScanCfg<KS>::RB, NDB = ScanCfg<KS>::NDB, DH = ScanCfg<KS>::DH, QW = ScanCfg<KS>::QW;
   // tile ring + chunk maxima [tile][row]: 4 x 32 KiB + 32 KiB (h 256) or 2 x 64 KiB + 16
   // KiB (h 512), one workgroup per CU
   __shared__ __attribute__((aligned(16))) char lds[SC_SLOTS * TI::BYTES + SC_TPS_MAX * SC_ROWS * 4];
@@ -141,7 +154,14 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
   const int nt = (int)(nch - t0 < tps ? nch - t0 : tps);
   if (nt <= 0) return;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const long row0 = (long)rt * SC_ROWS + wave * (SC_RB * 16);
+  const int qw = wave % QW, dh = wave / QW;  // query group, document part
+  const int db0 = dh * NDB;                  // this wave's first 16-document block
+  const long row0 = (long)rt * SC_ROWS + qw * (SC_RB * 16);
+  if (DH > 1) {  // the halves' chunk maxima meet in LDS: start from -inf (ordered before
+    // the first ds_max by tile 0's barrier)
+    for (int e = threadIdx.x; e < SC_TPS_MAX * SC_ROWS; e += SC_WAVES * 64) cms[e] = -FLT_MAX;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
   constexpr int h = 32 * KS;
   // The first two tiles are requested before the query rows, so their latency overlaps.
   ScanDma<KS> dm;
@@ -196,33 +216,46 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
     }
   };
   // Chunk maxima of tile t (masked form: positive -> -1, documents past nd -> -inf).
-  auto chunk_max = [&](const f32x4 (&a)[4][SC_RB], int t, bool masked) {
+  // the chunk maximum of (tile t, row) -> cms: stored, or max-ed with the other document
+  // part's (ds_max_f32 on the -inf initialised slot)
+  auto put_max = [&](int t, int qb, float m) {
+    if (lane < 16) {
+      float* dst = cms + t * SC_ROWS + qw * SC_RB * 16 + qb * 16 + lane;
+      if constexpr (DH == 1) {
+        *dst = m;
+      } else {
+        const uint32_t a = ttg::lds_addr_of(dst);
+        asm volatile("ds_max_f32 %0, %1" ::"v"(a), "v"(m) : "memory");
+      }
+    }
+  };
+  auto chunk_max = [&](const f32x4 (&a)[NDB][SC_RB], int t, bool masked) {
     const int n0 = (int)((t0 + t) * SC_COLS);
     const bool diag = label_off >= 0 && label_off + row0 < n0 + SC_COLS && n0 < label_off + row0 + SC_RB * 16;
 #pragma unroll
     for (int qb = 0; qb < SC_RB; ++qb) {
-      float v[16];
+      float v[4 * NDB];
 #pragma unroll
-      for (int db = 0; db < 4; ++db)
+      for (int db = 0; db < NDB; ++db)
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[db * 4 + r] = a[db][qb][r];
       if (masked) {
         const int lab = (int)(label_off + row0) + qb * 16 + (lane & 15) - n0;  // tile-relative
         const int lim = (int)(nd - n0);
 #pragma unroll
-        for (int db = 0; db < 4; ++db)
+        for (int db = 0; db < NDB; ++db)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int doc = db * 16 + 4 * (lane >> 4) + r;
+            const int doc = (db0 + db) * 16 + 4 * (lane >> 4) + r;
             if (diag && doc == lab) v[db * 4 + r] = -1.f;
             if (doc >= lim) v[db * 4 + r] = -FLT_MAX;
           }
       }
       float m = fmaxf(fmaxf(v[0], v[1]), v[2]);
 #pragma unroll
-      for (int j = 3; j < 15; j += 2) m = fmaxf(fmaxf(m, v[j]), v[j + 1]);
-      m = rowgroup_max4(fmaxf(m, v[15]));
-      if (lane < 16) cms[t * SC_ROWS + wave * SC_RB * 16 + qb * 16 + lane] = m;
+      for (int j = 3; j < 4 * NDB - 1; j += 2) m = fmaxf(fmaxf(m, v[j]), v[j + 1]);
+      m = rowgroup_max4(fmaxf(m, v[4 * NDB - 1]));
+      put_max(t, qb, m);
     }
   };
   // MFMAs of tile t into acc, with (EPI) the unmasked chunk maxima of tile t-1 (prev)
@@ -230,65 +263,69 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
   // the fragment reads of k-step ks+2, the 8 MFMAs of ks, then one slice of the epilogue,
   // so the LDS reads run two k-steps ahead and the epilogue VALU fills MFMA issue gaps
   // (hipcc otherwise sinks every read to just before its MFMA and clusters the VALU).
-  auto tile = [&](f32x4 (&acc)[4][SC_RB], const f32x4 (&prev)[4][SC_RB], int t, bool epi) {
+  auto tile = [&](f32x4 (&acc)[NDB][SC_RB], const f32x4 (&prev)[NDB][SC_RB], int t, bool epi) {
     const char* img = lds + (t % SC_SLOTS) * TI::BYTES;
 #pragma unroll
-    for (int db = 0; db < 4; ++db)
+    for (int db = 0; db < NDB; ++db)
 #pragma unroll
       for (int qb = 0; qb < SC_RB; ++qb) acc[db][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    uint4 fa[3][4];
+    // fragment ring: k-steps PF ahead
+    constexpr int PF = 2;
+    uint4 fa[PF + 1][NDB];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < PF; ++ks)
 #pragma unroll
-      for (int db = 0; db < 4; ++db)
-        fa[ks][db] = *reinterpret_cast<const uint4*>(img + TI::off(db * 16 + (lane & 15), ks * 4 + (lane >> 4)));
-    // epilogue slice i: query block i / 3; two half-maxima (documents 0-31, 32-63), then
-    // the 4-row-group reduction and the store
+      for (int db = 0; db < NDB; ++db)
+        fa[ks][db] =
+            *reinterpret_cast<const uint4*>(img + TI::off((db0 + db) * 16 + (lane & 15), ks * 4 + (lane >> 4)));
+    // epilogue slice i: query block i / NSQ; NDB / 2 partial maxima over two document
+    // blocks each, then the 4-row-group reduction and the store
+    constexpr int NSQ = NDB / 2 + 1;  // slices per query block
     float m = 0.f;
     auto slice = [&](int i) {
-      const int qb = i / 3, part = i % 3;
+      const int qb = i / NSQ, part = i % NSQ;
       if (qb >= SC_RB) return;
-      if (part < 2) {
+      if (part < NSQ - 1) {
         const f32x4 x = prev[2 * part][qb], y = prev[2 * part + 1][qb];
         const float hm =
             fmaxf(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])), fmaxf(fmaxf(y[0], y[1]), fmaxf(y[2], y[3])));
         m = part == 0 ? hm : fmaxf(m, hm);
       } else {
         m = rowgroup_max4(m);
-        if (lane < 16) cms[(t - 1) * SC_ROWS + wave * SC_RB * 16 + qb * 16 + lane] = m;
+        put_max(t - 1, qb, m);
       }
     };
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       dma_k(t, ks);
-      if (ks + 2 < KS) {
+      if (ks + PF < KS) {
 #pragma unroll
-        for (int db = 0; db < 4; ++db)
-          fa[(ks + 2) % 3][db] =
-              *reinterpret_cast<const uint4*>(img + TI::off(db * 16 + (lane & 15), (ks + 2) * 4 + (lane >> 4)));
+        for (int db = 0; db < NDB; ++db)
+          fa[(ks + PF) % (PF + 1)][db] = *reinterpret_cast<const uint4*>(
+              img + TI::off((db0 + db) * 16 + (lane & 15), (ks + PF) * 4 + (lane >> 4)));
       }
 #pragma unroll
-      for (int db = 0; db < 4; ++db)
+      for (int db = 0; db < NDB; ++db)
 #pragma unroll
         for (int qb = 0; qb < SC_RB; ++qb)
-          acc[db][qb] = ttg::mma<bf16_t>(fa[ks % 3][db], qa[qb][ks], acc[db][qb]);
+          acc[db][qb] = ttg::mma<bf16_t>(fa[ks % (PF + 1)][db], qa[qb][ks], acc[db][qb]);
       if (epi) slice(ks);
       __builtin_amdgcn_sched_barrier(0);
     }
     if (epi) {
 #pragma unroll
-      for (int i = KS; i < 3 * SC_RB; ++i) slice(i);
+      for (int i = KS; i < NSQ * SC_RB; ++i) slice(i);
     }
   };
-  f32x4 accA[4][SC_RB], accB[4][SC_RB];
+  f32x4 accA[NDB][SC_RB], accB[NDB][SC_RB];
   // Tiles holding a positive (label) column or documents past nd take the masked form.
   auto special = [&](int t) {
     const long n0 = (t0 + t) * SC_COLS;
     return (label_off >= 0 && label_off + row0 < n0 + SC_COLS && n0 < label_off + row0 + SC_RB * 16) ||
            n0 + SC_COLS > nd;
   };
-  auto step = [&](f32x4 (&cur)[4][SC_RB], const f32x4 (&prev)[4][SC_RB], int t) {  // t >= 1
+  auto step = [&](f32x4 (&cur)[NDB][SC_RB], const f32x4 (&prev)[NDB][SC_RB], int t) {  // t >= 1
     sync(t);
     if (special(t - 1)) {
       tile(cur, prev, t, false);
@@ -297,19 +334,31 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
       tile(cur, prev, t, true);
     }
   };
-  sync(0);
-  tile(accB, accA, 0, false);
-  int t = 1;
-  for (; t + 1 < nt; t += 2) {
-    step(accA, accB, t);
-    step(accB, accA, t + 1);
-  }
-  if (t < nt) {
-    step(accA, accB, t);
-    chunk_max(accA, t, special(t));
+  if constexpr (DH > 1) {
+    // document-split form: the 64-query fragments leave no registers for a second
+    // accumulator set, so each tile's maxima follow its own MFMAs (the partner wave on the
+    // SIMD keeps the matrix pipe busy meanwhile)
+    for (int t = 0; t < nt; ++t) {
+      sync(t);
+      tile(accA, accA, t, false);
+      chunk_max(accA, t, special(t));
+    }
   } else {
-    chunk_max(accB, t - 1, special(t - 1));
+    sync(0);
+    tile(accB, accA, 0, false);
+    int t = 1;
+    for (; t + 1 < nt; t += 2) {
+      step(accA, accB, t);
+      step(accB, accA, t + 1);
+    }
+    if (t < nt) {
+      step(accA, accB, t);
+      chunk_max(accA, t, special(t));
+    } else {
+      chunk_max(accB, t - 1, special(t - 1));
+    }
   }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's ds_max (inline asm: not counted by hipcc)
   __syncthreads();
   const long rbase = (long)rt * SC_ROWS;
   for (int e = threadIdx.x; e < SC_ROWS * nt; e += SC_WAVES * 64) {

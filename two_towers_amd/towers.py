@@ -201,6 +201,15 @@ def check_gru_status(wait: bool = True):
             "(env TT_GRU_FWD_XC=0) to use the row-owning kernel.")
 
 
+def _xs_selected() -> bool:
+    """Whether tt_gru_fwd's column-split form is gru_fwd_xs (option gru_fwd_xs; a library
+    without the option runs gru_fwd_xcp)."""
+    try:
+        return bool(_lib.get_option("gru_fwd_xs"))
+    except _lib.TTError:
+        return False
+
+
 def table_cols(table, x):
     return getattr(table, "real_cols", table.shape[1])
 
@@ -267,7 +276,7 @@ def _gru_layer_fwd(cfg, xs, K, ldx, packs, layer, B, T, seeds, want_x1, ws):
         else _lib.load().tt_gru_fwd_launches(dtype_code(dt), T, H)
     per = esz * (8 + (1 if want_x1 else 0)) + (0 if nl == 1 else esz + 8)
     if nl == 1 and ws is not None:
-        form = "gru_fwd_xs" if H == 512 and _lib.get_option("gru_fwd_xs") else "gru_fwd_xcp"
+        form = "gru_fwd_xs" if H == 512 and _xs_selected() else "gru_fwd_xcp"
         kname = f"{form}<{H}, {'true' if want_x1 and cfg.drop_p > 0 else 'false'}>"
     elif nl == 1:
         kname = "gru_fwd_seq<"

@@ -22,7 +22,7 @@ for d in sorted(glob.glob(sys.argv[1] + "/libtt*/")):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
         if "hn_" in r["Kernel_Name"]:
-            name = r["Kernel_Name"].split("(")[0].split("::")[-1]
+            name = r["Kernel_Name"].split("::")[-1].split("(")[0]
             agg[(name, r["Grid_Size_X"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     for (name, grid), v in sorted(agg.items()):
         v.sort()

@@ -401,6 +401,9 @@ TT_DEV void epi_direct(const GemmArgs& g, const f32x4 (&acc)[8][4], TO* C, const
 // cover all panels, so each A row is fetched into an XCD's L2 once and read by the 16
 // (or 32) panels' workgroups. Same MFMA (16x16x32, B fragment first: the transposed
 // accumulate of the persistent kernel), same k order from zero: bit-identical to it.
+#ifndef BRES_DIAG  // timing-only diagnostic switches of gemm_bres (results wrong): 1 no output stores
+#define BRES_DIAG 0
+#endif
 constexpr int BR_COLS = 192;  // B panel columns per workgroup
 template <int NKS>  // k-steps of 32
 __global__ __launch_bounds__(512, 1) void gemm_bres(GemmArgs g, int npan, int nbatch) {
@@ -500,8 +503,12 @@ __global__ __launch_bounds__(512, 1) void gemm_bres(GemmArgs g, int npan, int nb
         const auto s0 = __builtin_amdgcn_permlane16_swap(w[0][0], w[1][0], false, false);
         const auto s1 = __builtin_amdgcn_permlane16_swap(w[0][1], w[1][1], false, false);
         const int cs = n0 + 16 * (2 * jp + (q & 1)) + 8 * (q >> 1);
+#if BRES_DIAG & 1  // timing only: no stores (the packed values stay live)
+        asm volatile("" ::"v"(s0[0]), "v"(s1[0]), "v"(s0[1]), "v"(s1[1]), "v"(ok));
+#else
         if (ok)
           *reinterpret_cast<uint4*>(C + (long)(g0 + row) * g.ldc + cs) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+#endif
       }
     }
   }

@@ -1761,6 +1761,11 @@ template <int H, bool DROP>
 __global__ __launch_bounds__(xs::NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void gru_fwd_xs(FwdArgs a, XcWs ws) {
   using C = xc::Cfg<H>;
   constexpr int M = C::M, NKT = C::NKT, QPW = C::QPW;
+#ifdef TT_DIAG  // timing only (results wrong): 1 no output stores, 2 no G loads, 4 no exchange
+  const int dbg = a.dbg;  // loads (h = 0), 8 no MFMAs, 16 no gate arithmetic, 32 no counter waits
+#else
+  constexpr int dbg = 0;
+#endif
   __shared__ __attribute__((aligned(16))) char lds[xs::Cfg<H>::LDS];
   char* slots = lds;
   float* stgb = reinterpret_cast<float*>(lds + 2 * C::SLOT);  // [2][32 rows][192] fp32
@@ -1818,6 +1823,15 @@ __global__ __launch_bounds__(xs::NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2)
     // gates of one chunk from h slot `sl` into gate buffer `gb` (C^T: 4 units of a row per lane)
     auto chunk = [&](const char* sl, float* gb) {
       f32x4 acc[2][3];
+      if (dbg & 8) {
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+          for (int g = 0; g < 3; ++g)
+            *reinterpret_cast<f32x4*>(gb + stg_off(rb * 16 + (lane & 15), g * 64 + 16 * wave + 4 * (lane >> 4))) =
+                f32x4{0.f, 0.f, 0.f, 0.f};
+        return;
+      }
       const char* base = sl + lane * 16;
       auto frag = [&](int kt, int rb) { return *reinterpret_cast<const tt_u32x4*>(base + (kt * 2 + rb) * 1024); };
 #pragma unroll
@@ -1882,11 +1896,12 @@ __global__ __launch_bounds__(xs::NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2)
     const uint32_t og = c * xc::CR + cr < q.nrow ? (uint32_t)(((c * xc::CR + cr) * T_ + q.t) * (int)a.ldg + j) * 2u
                                                   : xc::OOB;
 #pragma unroll
-    for (int g = 0; g < 3; ++g) gx[g] = __builtin_amdgcn_raw_buffer_load_b128(rG, (int)og, g * H * 2, XC_G_AUX);
+    for (int g = 0; g < 3; ++g)
+      gx[g] = (dbg & 2) ? tt_u32x4{0u, 0u, 0u, 0u} : __builtin_amdgcn_raw_buffer_load_b128(rG, (int)og, g * H * 2, XC_G_AUX);
   };
   tt_u32x4 hv[QPW];
   auto load_h = [&](const Step& q, int qidx, int c) {
-    if (q.s == 0) {
+    if (q.s == 0 || (dbg & 4)) {
 #pragma unroll
       for (int p = 0; p < QPW; ++p) hv[p] = tt_u32x4{0u, 0u, 0u, 0u};
     } else {
@@ -1941,7 +1956,11 @@ __global__ __launch_bounds__(xs::NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float hp = first ? 0.f : st[c][e];
-          gru_cell(xr[e], xz[e], xn[e], lr[e], lz[e], ln[e], bn[e], hp, y[e], sr[e], sz[e], sn[e], sg[e]);
+          if (dbg & 16) {
+            y[e] = xr[e] + lr[e] + hp; sr[e] = xz[e] + lz[e]; sz[e] = xn[e] + ln[e]; sn[e] = bn[e]; sg[e] = hp;
+          } else {
+            gru_cell(xr[e], xz[e], xn[e], lr[e], lz[e], ln[e], bn[e], hp, y[e], sr[e], sz[e], sn[e], sg[e]);
+          }
           st[c][e] = y[e];
         }
         const uint4 yb = pack8bf(y);
@@ -1949,8 +1968,9 @@ __global__ __launch_bounds__(xs::NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2)
         else st16_buf_sc1(rdst_h, (uint32_t)(rr * H + j) * 2u, 0, yb);
         asm volatile("" ::: "memory");  // exactly 6 stores follow (the publish below waits for the rest)
         const int lrow = rr * T_ + t;
-        const uint32_t oy = ok ? (uint32_t)(lrow * (int)a.ldy + j) * 2u : xc::OOB;
-        const uint32_t os = ok ? (uint32_t)(lrow * 4 * H + j) * 2u : xc::OOB;
+        const bool okd = ok && !(dbg & 1);
+        const uint32_t oy = okd ? (uint32_t)(lrow * (int)a.ldy + j) * 2u : xc::OOB;
+        const uint32_t os = okd ? (uint32_t)(lrow * 4 * H + j) * 2u : xc::OOB;
         st16_buf_aux<XC_OUT_AUX>(rY, (int)oy, yb);
         st16_buf_aux<XC_OUT_AUX>(rS, (int)os, pack8bf(sr));
         st16_buf_aux<XC_OUT_AUX>(rS, (int)(os + 2u * H), pack8bf(sz));
@@ -1975,7 +1995,7 @@ __global__ __launch_bounds__(xs::NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2)
       }
       if (c + 3 < xc::NCH) load_h(cur, idx, c + 3);
       else if (has_next) load_h(nxt, idx + 1, c + 3 - xc::NCH);
-      if (vt == 0) {
+      if (vt == 0 && !(dbg & 32)) {
         if (c == 0 && idx > 0) xc_wait(cntB, (unsigned)(M * idx), ws);
         if (c == 4 && has_next) xc_wait(cntA, (unsigned)(M * (idx + 1)), ws);
       }

@@ -443,9 +443,10 @@ __global__ __launch_bounds__(256) void margin_fwd_kernel(const float* __restrict
 //                           it, in ascending group order, then ddn[document] += the sum.
 constexpr int MB_ENT = 2048;
 
-// rows per group: the largest power of two <= 64 with R (k + 1) <= MB_ENT
+// rows per group: the largest power of two <= 32 with R (k + 1) <= MB_ENT (32: 256 groups at
+// B 8192, one per CU; 64 measured 80 us for the group pass at configs[2])
 inline int margin_group_rows(int k) {
-  int r = 64;
+  int r = 32;
   while (r > 1 && (long)r * (k + 1) > MB_ENT) r >>= 1;
   return r;
 }
@@ -481,6 +482,9 @@ __global__ __launch_bounds__(256) void margin_rows_kernel(const float* __restric
   if (lane == 0) coef[row] = make_float2(gp, gn);
 }
 
+// q rows of a group staged in LDS for the partial sums when they fit (h <= 512 at R 64)
+constexpr int MG_QS_BYTES = 64 * 512 * 4;
+
 __global__ __launch_bounds__(256) void margin_group_kernel(const float* __restrict__ qn, long bq, int h,
                                                            long label_off, const int32_t* __restrict__ idx, int k,
                                                            const float2* __restrict__ coef, int R, int G,
@@ -488,11 +492,17 @@ __global__ __launch_bounds__(256) void margin_group_kernel(const float* __restri
   __shared__ unsigned long long key[MB_ENT];  // document << 32 | entry; unused = all ones
   __shared__ int head[MB_ENT];                // sorted position of slot u's first entry
   __shared__ int wsum[256];
+  __shared__ __attribute__((aligned(16))) float qs[MG_QS_BYTES / 4];
   const int g = blockIdx.x;
   const long r0 = (long)g * R;
   const int nr = (int)(bq - r0 < R ? bq - r0 : R);
   const int kp = k + 1;  // entry 0 of a row: its positive; 1..k: its negatives
   const int ne = nr * kp;
+  __shared__ float2 cf[64];  // the rows' coefficients (R <= 64)
+  const bool staged = (long)nr * h * 4 <= MG_QS_BYTES;
+  if (staged)
+    for (int e = threadIdx.x; e < nr * h; e += 256) qs[e] = qn[r0 * h + e];
+  if (threadIdx.x < nr) cf[threadIdx.x] = coef[r0 + threadIdx.x];
   int n2 = 2;
   while (n2 < ne) n2 <<= 1;
   for (int e = threadIdx.x; e < n2; e += 256) {
@@ -536,40 +546,49 @@ __global__ __launch_bounds__(256) void margin_group_kernel(const float* __restri
     __syncthreads();
   }
   int u = wsum[threadIdx.x] - cnt;
+  __shared__ int s_nh, s_nv;  // slots; valid keys (they sort first)
   for (int i = p0; i < p0 + per && i < n2; ++i) {
     const unsigned long long v = key[i];
-    if (v != ~0ull && (i == 0 || (key[i - 1] >> 32) != (v >> 32))) head[u++] = i;
+    if (v == ~0ull) continue;
+    if (i == 0 || (key[i - 1] >> 32) != (v >> 32)) head[u++] = i;
+    if (i + 1 == n2 || key[i + 1] == ~0ull) s_nv = i + 1;
   }
+  if (threadIdx.x == 255) s_nh = wsum[255];
+  if (threadIdx.x == 0 && key[0] == ~0ull) s_nv = 0;
   __syncthreads();
-  const int nh = wsum[255];
+  const int nh = s_nh, nv = s_nv;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float* Pg = P + (long)g * R * kp * h;
-  for (int s = wave; s < nh; s += 4) {
-    const int i0 = head[s];
+  // one wave per slot: the coefficient-weighted sum of the slot's q rows in entry order
+  // (from LDS when staged), written as the group's partial row
+  for (int sl = wave; sl < nh; sl += 4) {
+    const int i0 = head[sl], i1 = sl + 1 < nh ? head[sl + 1] : nv;
     const unsigned doc = (unsigned)(key[i0] >> 32);
     for (int c0 = 0; c0 < h; c0 += 256) {
       float acc[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int i = i0; i < n2 && key[i] != ~0ull && (unsigned)(key[i] >> 32) == doc; ++i) {
+      for (int i = i0; i < i1; ++i) {
         const int e = (int)(key[i] & 0xffffffffu);
         const int rl = e / kp;
-        const float w = e - rl * kp == 0 ? coef[r0 + rl].x : coef[r0 + rl].y;
-        const float* q = qn + (r0 + rl) * h;
+        const float w = e - rl * kp == 0 ? cf[rl].x : cf[rl].y;
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const int c = c0 + lane + 64 * m;
-          if (c < h) acc[m] += w * q[c];
+          if (c < h) acc[m] += w * (staged ? qs[rl * h + c] : qn[(r0 + rl) * h + c]);
         }
       }
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const int c = c0 + lane + 64 * m;
-        if (c < h) Pg[(long)s * h + c] = acc[m];
+        if (c < h) Pg[(long)sl * h + c] = acc[m];
       }
     }
-    if (lane == 0) SM[(long)doc * G + g] = s + 1;
+    if (lane == 0) SM[(long)doc * G + g] = sl + 1;
   }
 }
 
+// One wave per document: the partials of the groups that hold it, added in ascending
+// group order; their loads are issued eight at a time before the adds (independent
+// rows), so a document's chain costs one load latency per eight groups.
 __global__ __launch_bounds__(256) void margin_combine_kernel(const int* __restrict__ SM, int G,
                                                              const float* __restrict__ P, long gstride, int h,
                                                              long nd, float* __restrict__ ddn) {
@@ -585,16 +604,30 @@ __global__ __launch_bounds__(256) void margin_combine_kernel(const int* __restri
     for (int g0 = 0; g0 < G; g0 += 64) {
       const int s = g0 + lane < G ? sm[g0 + lane] : 0;
       unsigned long long mask = __builtin_amdgcn_ballot_w64(s != 0);
-      while (mask) {  // groups in ascending order
-        const int b = __builtin_ctzll(mask);
-        mask &= mask - 1;
-        const int slot = __builtin_amdgcn_readlane(s, b) - 1;
-        const float* p = P + (long)(g0 + b) * gstride + (long)slot * h;
+      while (mask) {  // groups in ascending order, eight loads in flight
+        constexpr int NB = 8;
+        float v[NB][4];
+        int n = 0;
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const int c = c0 + lane + 64 * m;
-          if (c < h) acc[m] += p[c];
+        for (int u = 0; u < NB; ++u) {
+          if (mask) {
+            const int b = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            const int slot = __builtin_amdgcn_readlane(s, b) - 1;
+            const float* p = P + (long)(g0 + b) * gstride + (long)slot * h;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+              const int c = c0 + lane + 64 * m;
+              v[u][m] = c < h ? p[c] : 0.f;
+            }
+            n = u + 1;
+          }
         }
+#pragma unroll
+        for (int u = 0; u < NB; ++u)
+          if (u < n)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) acc[m] += v[u][m];
       }
     }
 #pragma unroll

@@ -29,11 +29,11 @@
 
 namespace {
 
-#ifndef HN_SPREAD  // 0: a tile's due DMAs in one burst at its first k-step (the round-3 form)
-#define HN_SPREAD 1
+#ifndef HN_SPREAD  // 1: a tile's due DMAs spread over its k-steps (measured slower: 44.6 vs 38.2 us, the
+#define HN_SPREAD 0  // last pieces then land one tile before their wait instead of two); 0: one burst
 #endif
-#ifndef HN_DSPLIT  // h 256: 1 = every wave takes all 64 documents of a tile for 32 queries
-#define HN_DSPLIT 2  // (the round-3 form); 2 = half the documents for 64 queries
+#ifndef HN_DSPLIT  // h 256: 1 = every wave takes all 64 documents of a tile for 32 queries (the
+#define HN_DSPLIT 1  // round-3 form, 37.7 us); 2 = half the documents for 64 queries (41.9 us, r05_hn_scan_ab)
 #endif
 constexpr int SC_COLS = 64;     // document columns per tile (= per chunk)
 constexpr int SC_TPS_MAX = 32;  // tiles per workgroup (chunk-max staging)
@@ -188,10 +188,8 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
   // With two slots (h 512) every tile is retired alone and the next one requested into
   // the slot its predecessor freed.
   // The DMAs of the tiles that become due at tile t's barrier (t + 1 with two slots; t + 2
-  // and t + 3 at the start of a pair) are spread over tile t's k-steps, NPK per k-step,
-  // instead of issued in one burst after the barrier: every wave of the CU reaches that
-  // barrier together, so a burst (8 pieces per wave at h 256, ~100 cycles of issue each)
-  // left the matrix pipes idle. They still all land before the next wait retires them.
+  // and t + 3 at the start of a pair) are issued at tile t's first k-step (HN_SPREAD 1:
+  // spread over its k-steps, NPK per k-step -- slower, profiles/r05_hn_scan_ab_e.txt).
   constexpr int NPD = SC_SLOTS == 2 ? TI::DPW : 2 * TI::DPW;  // pieces due per DMA tile
   constexpr int NPK = HN_SPREAD ? (NPD + KS - 1) / KS : NPD;  // pieces per k-step (0: all at k-step 0)
   auto sync = [&](int t) {

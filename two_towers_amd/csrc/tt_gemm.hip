@@ -404,6 +404,12 @@ TT_DEV void epi_direct(const GemmArgs& g, const f32x4 (&acc)[8][4], TO* C, const
 #ifndef BRES_DIAG  // timing-only diagnostic switches of gemm_bres (results wrong): 1 no output stores
 #define BRES_DIAG 0
 #endif
+#ifndef BRES_STORE  // output store policy of gemm_bres: 0 plain, 1 write-through (sc1), 2 non-temporal
+#define BRES_STORE 0
+#endif
+#ifndef BRES_STAG  // waves 4-7 start BRES_STAG x 64 cycles late (0: together)
+#define BRES_STAG 0
+#endif
 constexpr int BR_COLS = 192;  // B panel columns per workgroup
 template <int NKS>  // k-steps of 32
 __global__ __launch_bounds__(512, 1) void gemm_bres(GemmArgs g, int npan, int nbatch) {
@@ -447,6 +453,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bres(GemmArgs g, int npan, int nb
     const uint32_t off = t < ntl && g0 + row < g.M ? (uint32_t)((row * (int)g.lda + ks * 32 + q * 8) * 2) : 0x80000000u;
     return ld16_buf(ra, off, 0);
   };
+  if (BRES_STAG > 0 && wave >= 4) __builtin_amdgcn_s_sleep(BRES_STAG);
   uint4 ar[PD][2];
   int t = wave;
 #pragma unroll
@@ -506,8 +513,15 @@ __global__ __launch_bounds__(512, 1) void gemm_bres(GemmArgs g, int npan, int nb
 #if BRES_DIAG & 1  // timing only: no stores (the packed values stay live)
         asm volatile("" ::"v"(s0[0]), "v"(s1[0]), "v"(s0[1]), "v"(s1[1]), "v"(ok));
 #else
-        if (ok)
-          *reinterpret_cast<uint4*>(C + (long)(g0 + row) * g.ldc + cs) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        if (ok) {
+          const uint4 v = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+          if constexpr (BRES_STORE == 0) {
+            *reinterpret_cast<uint4*>(C + (long)(g0 + row) * g.ldc + cs) = v;
+          } else {
+            const __amdgpu_buffer_rsrc_t rc = tt_rsrc(C + (long)g0 * g.ldc);
+            st16_buf_aux<BRES_STORE == 1 ? 16 : 2>(rc, (int)(((long)row * g.ldc + cs) * 2), v);
+          }
+        }
 #endif
       }
     }

@@ -1747,6 +1747,9 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
 // so each SIMD's matrix pipe and vector issue are fed by different waves (MI355X_MICROARCH.md
 // "Two waves per SIMD"), with ONE barrier per chunk. The MFMA sequence per chunk and the
 // cell are gru_fwd_xcp's (same k order from zero, gru_cell): bit-identical outputs.
+#ifndef XS_GA  // gru_fwd_xs: chunks of gate inputs requested ahead
+#define XS_GA 1
+#endif
 namespace xs {
 constexpr int NT = 512;
 template <int H>
@@ -1913,8 +1916,13 @@ __global__ __launch_bounds__(xs::NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2)
   float st[xc::NCH][8];  // fp32 state of this thread's (row, 8 units) in each chunk of the round
   Step cur = step_of(0);
   __amdgpu_buffer_rsrc_t rGc = g_rsrc(cur);
-  tt_u32x4 gq[2][3];
-  load_g(cur, rGc, 0, gq[0]);
+  // gate inputs XS_GA chunks ahead, in a ring of GR sets (a power of two > XS_GA, so that a
+  // chunk's set is fixed at compile time: 8 chunks per step)
+  constexpr int GR = XS_GA < 2 ? 2 : 4;
+  static_assert(XS_GA >= 1 && XS_GA < GR && xc::NCH % GR == 0, "gate-input ring");
+  tt_u32x4 gq[GR][3];
+#pragma unroll
+  for (int c = 0; c < XS_GA; ++c) load_g(cur, rGc, c, gq[c]);
 #pragma unroll
   for (int p = 0; p < QPW; ++p) hv[p] = tt_u32x4{0u, 0u, 0u, 0u};  // step 0, chunk 2
   __syncthreads();  // the matrix waves' chunk 0
@@ -1932,14 +1940,15 @@ __global__ __launch_bounds__(xs::NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2)
     const bool first = cur.s == 0;
 #pragma unroll
     for (int c = 0; c < xc::NCH; ++c) {
-      if (c + 1 < xc::NCH) load_g(cur, rGc, c + 1, gq[(c + 1) & 1]);
-      else if (has_next) load_g(nxt, rGn, 0, gq[0]);
+      const int gslot = c % GR, gnext = (c + XS_GA) % GR;
+      if (c + XS_GA < xc::NCH) load_g(cur, rGc, c + XS_GA, gq[gnext]);
+      else if (has_next) load_g(nxt, rGn, c + XS_GA - xc::NCH, gq[gnext]);
       {
         const int rr = c * xc::CR + cr;
         const bool ok = rr < cur.nrow;
         const float* gb = stgb + (c & 1) * (xc::STG / 4);
         float xr[8], xz[8], xn[8], lr[8], lz[8], ln[8], y[8], sr[8], sz[8], sn[8], sg[8];
-        const tt_u32x4(&gcur)[3] = gq[c & 1];
+        const tt_u32x4(&gcur)[3] = gq[gslot];
         unpack8(make_uint4(gcur[0][0], gcur[0][1], gcur[0][2], gcur[0][3]), xr);
         unpack8(make_uint4(gcur[1][0], gcur[1][1], gcur[1][2], gcur[1][3]), xz);
         unpack8(make_uint4(gcur[2][0], gcur[2][1], gcur[2][2], gcur[2][3]), xn);

@@ -81,7 +81,13 @@ int tt_colsum(const float* x, long rows, int cols, long ld, float* out, int accu
  * splits > 1 splits K across workgroups: fp32 partials go to splitk_ws
  * (tt_gemm_ws_size floats) and are reduced into C; relu/dropout unsupported then.
  * out_dtype is TT_DT_F32 or dtype. Any m, n, k; operand base pointers and leading
- * dimensions must be 16-byte aligned (lda * sizeof(dtype) % 16 == 0). */
+ * dimensions must be 16-byte aligned (lda * sizeof(dtype) % 16 == 0).
+ * Library path (option gemm_lt, default 1): a one-split bf16 -> bf16 problem with both
+ * operands K-contiguous, alpha 1, no accumulate / relu / dropout / shift / a_split,
+ * k >= 512 and m >= 65536 (the layer-1 input projection) runs on hipBLASLt when the caller
+ * passes splitk_ws with tt_gemm_ws_size(m, n, nbatch, 1) floats (TT_GEMM_LT_WS bytes);
+ * with splitk_ws NULL it runs on the hand-written kernels. */
+#define TT_GEMM_LT_WS (64L << 20)
 typedef struct {
   const void* a[4];
   const void* b[4];
@@ -101,6 +107,8 @@ int tt_gemm(int dtype, int out_dtype, int a_kouter, int b_kouter, int m, int n, 
             const tt_gemm_batch* batch, int nbatch, long lda, long ldb, long ldc, float alpha,
             int beta_accum, int relu, int seq_t, uint32_t drop_seed, float drop_p, int splits,
             float* splitk_ws, void* stream);
+/* fp32 elements of splitk_ws: the split partials for splits > 1; for splits = 1 the
+ * library path's workspace (TT_GEMM_LT_WS bytes) when m >= 65536, else 0. */
 long tt_gemm_ws_size(int m, int n, int nbatch, int splits);
 /* Heuristic split count for a (m, n, k, nbatch) problem. */
 int tt_gemm_pick_splits(int m, int n, int k, int nbatch);

@@ -170,6 +170,10 @@ def test_split_k_picker_fills_the_chip():
         assert s > 1, (m, n, k, s)
         assert k // s >= 64 * 8 or s == 1
     assert lib.tt_gemm_pick_splits(524288, 3072, 1024, 2) == 1
+    # one-split calls: the library path's workspace (TT_GEMM_LT_WS = 64 MiB) from M 65536 on
+    assert lib.tt_gemm_ws_size(524288, 3072, 2, 1) == (64 << 20) // 4
+    assert lib.tt_gemm_ws_size(65535, 3072, 2, 1) == 0
+    assert lib.tt_gemm_ws_size(1536, 1024, 4, 8) == 1536 * 1024 * 4 * 8
     assert lib.tt_gru_fwd_launches(1, 64, 512) == 1 and lib.tt_gru_fwd_launches(0, 64, 512) == 64
 
 

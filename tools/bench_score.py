@@ -26,7 +26,7 @@ def timed(f, iters):
     return s.elapsed_time(e) / iters
 
 
-def hardneg(B, nd, h, k, dt, iters):
+def hardneg(B, nd, h, k, dt, iters, flush_mb=0):
     lib = _lib.load()
     g = torch.Generator(device="cuda").manual_seed(5)
     q = torch.nn.functional.normalize(torch.randn(B, h, device="cuda", generator=g), dim=1).to(dt)
@@ -36,6 +36,12 @@ def hardneg(B, nd, h, k, dt, iters):
     st = torch.cuda.current_stream().cuda_stream
     f = lambda: call("tt_hardneg_topk", dtype_code(dt), q.data_ptr(), B, d.data_ptr(), nd, h, 0, k, idx.data_ptr(),
                      None, ws.data_ptr(), st)
+    if flush_mb:  # a copy of flush_mb MiB before every call evicts the L2s and the MALL (the event time
+        # then includes the copy: read the scan's own duration from a kernel trace)
+        src = torch.empty(flush_mb << 20, dtype=torch.uint8, device="cuda")
+        dst = torch.empty_like(src)
+        f0 = f
+        f = lambda: (dst.copy_(src), f0())
     ms = timed(f, iters)
     tf = 2.0 * B * nd * h / (ms * 1e-3) / 1e12
     return {"op": "hardneg_topk", "B": B, "nd": nd, "h": h, "k": k, "dtype": str(dt)[6:], "ms": round(ms, 4),
@@ -81,6 +87,7 @@ if __name__ == "__main__":
     ap.add_argument("--ops", default="hardneg,infonce")
     ap.add_argument("--hn-shapes", default="8192x8192x256,8192x65536x256,8192x8192x512",
                     help="hard-negative shapes B x N x h")
+    ap.add_argument("--flush-mb", type=int, default=0, help="copy this many MiB before every hard-negative call")
     ap.add_argument("--variants", default="", help='hard-negative option sets, e.g. "wide=hn_wide=1;map=hn_map=1"')
     a = ap.parse_args()
     bf = torch.bfloat16
@@ -95,7 +102,7 @@ if __name__ == "__main__":
                 with contextlib.ExitStack() as es:
                     for k, v in opts.items():
                         es.enter_context(_lib.option(k, v))
-                    r = hardneg(B, nd, h, 5, bf, a.iters)
+                    r = hardneg(B, nd, h, 5, bf, a.iters, a.flush_mb)
                 r["variant"] = name
                 print(json.dumps(r), flush=True)
     if "infonce" in a.ops:

@@ -14,6 +14,7 @@ SHAPES = {  # name: (m, n, k, a_kouter, b_kouter, nbatch, out_bf16)
     "input_proj_l0": (524288, 3072, 320, 0, 0, 2, 1),  # Ep 320 since round 2 (304 before)
     "dgrad_l1": (524288, 1024, 3072, 0, 1, 1, 1),
     "wgrad_ih1": (1536, 1024, 524288, 1, 1, 4, 0),
+    "wgrad_ih0": (1536, 320, 524288, 1, 1, 4, 0),  # N = Ep 320: two 256-column tiles, the second a quarter full
     "wgrad_hh": (1536, 512, 524288, 1, 1, 4, 0),
     "square8k": (8192, 8192, 8192, 0, 0, 1, 1),
     # diagnostics: the round-1 16-byte padding; the l1 FLOPs with a B small enough for L2

@@ -290,3 +290,25 @@ def test_gemm_library_path_input_projection():
         assert rel_err(outs[1][i][rows].float(), ref) < 8e-3
         assert rel_err(outs[1][i].float(), outs[0][i].float()) < 8e-3
         assert not torch.isnan(outs[1][i]).any()
+
+
+@pytest.mark.parametrize("m", [320, 296, 384, 400, 64])
+@pytest.mark.parametrize("akout,bkout", [(1, 1), (0, 0)])
+def test_gemm_tail_tile_idle_wave_row(m, akout, bkout):
+    """256x256 tiles whose second wave row lies wholly past M (M mod 256 in (0, 128]) skip
+    that row's MFMAs (tt_gemm_core.h Loop8::quad, mm = false): the layer-0 dW_ih^T shape
+    (M = Ep 320, N = 3H, both operands K-outer, split-K, fp32 out) and ragged neighbours
+    (tail 40, 128 exactly, 144: both rows live; M 64: one tile), against fp32 math."""
+    dt = torch.bfloat16
+    n, k = 1536, 8192
+    g = torch.Generator().manual_seed(71 + m)
+    A = torch.randn(m, k, generator=g).to(dt)
+    B = torch.randn(n, k, generator=g).to(dt)
+    Ad = (A.t().contiguous() if akout else A).to(DEV)
+    Bd = (B.t().contiguous() if bkout else B).to(DEV)
+    C = torch.full((m, n), float("nan"), device=DEV)
+    ops.gemm([Ad], [Bd], [C], m=m, n=n, k=k, lda=m if akout else k, ldb=n if bkout else k, ldc=n,
+             a_kouter=bool(akout), b_kouter=bool(bkout), dtype=dt, out_dtype=torch.float32)
+    ref = A.float().to(DEV) @ B.float().to(DEV).t()
+    assert not torch.isnan(C).any()
+    assert rel_err(C, ref) < 1e-5, rel_err(C, ref)

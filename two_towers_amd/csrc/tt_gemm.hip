@@ -148,16 +148,20 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_kernel(GemmArgs g) {
   const int kt0 = s * g.kt_per_split;
   const int kt1 = min(nk, kt0 + g.kt_per_split);
 
+  // 8-phase loop: a wave row whose 128 tile rows all lie past M skips its MFMAs (tail tiles)
+  constexpr bool L8T = DMA && TBM == 256 && TBN == 256 && WGM == 2 && WGN == 4;
+  const bool mm = !L8T || __builtin_amdgcn_readfirstlane((int)(m0 + (int)(threadIdx.x >> 8) * 128 < g.M));
+  auto lrun = [&](const auto& la, const auto& lb) {
+    if constexpr (L8T) ML::run(la, lb, g.K, kt0, kt1, lds, acc, mm);
+    else ML::run(la, lb, g.K, kt0, kt1, lds, acc);
+  };
   auto run = [&](const auto& la) {
     if constexpr (!BKO) {
-      ttg::KCPlain<T> lb{B, g.ldb, n0, g.N};
-      ML::run(la, lb, g.K, kt0, kt1, lds, acc);
+      lrun(la, ttg::KCPlain<T>{B, g.ldb, n0, g.N});
     } else if constexpr (SHIFT) {
-      ttg::KOShift<T> lb{B, g.ldb, n0, g.N - n0, g.seq_t, g.bshift[bi]};
-      ML::run(la, lb, g.K, kt0, kt1, lds, acc);
+      lrun(la, ttg::KOShift<T>{B, g.ldb, n0, g.N - n0, g.seq_t, g.bshift[bi]});
     } else {
-      ttg::KOPlain<T> lb{B, g.ldb, n0, g.N - n0};
-      ML::run(la, lb, g.K, kt0, kt1, lds, acc);
+      lrun(la, ttg::KOPlain<T>{B, g.ldb, n0, g.N - n0});
     }
   };
   if constexpr (AKO) {

@@ -770,23 +770,29 @@ struct Loop8 {
   using Half = std::conditional_t<BUF && !L::KSPLIT && (!L::SHIFTED || TT_SHIFT_BUF),
                                   std::conditional_t<L::SHIFTED, SHalf<KO, L>, BHalf<KO, L>>, PHalf<KO, L>>;
 
-  TT_DEV static void quad(int mi, int ni, const uint4 (&fa)[2][4], const uint4 (&fb)[2][4], f32x4 (&acc)[TM][TN]) {
+  // mm (wave-uniform): false for a wave whose 128 tile rows all lie past M (the second wave
+  // row of a tail tile with <= 128 rows): it keeps its DMA share and barriers, skips its MFMAs
+  TT_DEV static void quad(int mi, int ni, const uint4 (&fa)[2][4], const uint4 (&fb)[2][4], f32x4 (&acc)[TM][TN],
+                          bool mm = true) {
     __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_s_setprio(1);
+    if (mm) {
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[4 * mi + i][2 * ni + j] = CT ? mma<T>(fb[ks][2 * ni + j], fa[ks][i], acc[4 * mi + i][2 * ni + j])
-                                           : mma<T>(fa[ks][i], fb[ks][2 * ni + j], acc[4 * mi + i][2 * ni + j]);
-    __builtin_amdgcn_s_setprio(0);
+          for (int j = 0; j < 2; ++j)
+            acc[4 * mi + i][2 * ni + j] = CT ? mma<T>(fb[ks][2 * ni + j], fa[ks][i], acc[4 * mi + i][2 * ni + j])
+                                             : mma<T>(fa[ks][i], fb[ks][2 * ni + j], acc[4 * mi + i][2 * ni + j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
     __builtin_amdgcn_s_barrier();
   }
 
   template <class LA, class LB>
-  TT_DEV static void run(const LA& la, const LB& lb, int K, int kt0, int kt1, char* lds, f32x4 (&acc)[TM][TN]) {
+  TT_DEV static void run(const LA& la, const LB& lb, int K, int kt0, int kt1, char* lds, f32x4 (&acc)[TM][TN],
+                         bool mm = true) {
     if (kt0 >= kt1) return;
     const int wave = threadIdx.x >> 6;
     const int wr = wave >> 2, bh = (wave & 3) >> 1, bc = (wave & 1) * 64;
@@ -798,7 +804,8 @@ struct Loop8 {
     pb0.init(lb, kt0, kt1, K, 0);
     pb1.init(lb, kt0, kt1, K, 128);
     if constexpr (A3) {
-      run3(kt1 - kt0, lds, base, pa0, pa1, pb0, pb1, acc);
+      if (mm) run3<true>(kt1 - kt0, lds, base, pa0, pa1, pb0, pb1, acc);
+      else run3<false>(kt1 - kt0, lds, base, pa0, pa1, pb0, pb1, acc);
       return;
     }
     pa0.issue(0, base);
@@ -887,7 +894,7 @@ struct Loop8 {
   // columns 0-31 and restages A0 of r+2, P2 reads B columns 32-63 and restages A1 of r+2,
   // P3 reads A rows 64-127, P4 restages both B halves of r+2 into B's current slot and
   // waits for K-tile r+1 with the 8 youngest DMAs (A and B of r+2) still in flight.
-  template <class HA, class HB>
+  template <bool MM, class HA, class HB>
   TT_DEV static void run3(int nk, char* lds, uint32_t base, const HA& pa0, const HA& pa1, const HB& pb0, const HB& pb1,
                           f32x4 (&acc)[TM][TN]) {
     const int wave = threadIdx.x >> 6;
@@ -914,26 +921,32 @@ struct Loop8 {
       const char* ia = lds + as * (2 * HALF) + wr * HALF;
       const char* ib = lds + BOFF + bs * (2 * HALF) + bh * HALF;
       const uint32_t anx = base + (uint32_t)an * (2 * HALF), bcur = base + BOFF + (uint32_t)bs * (2 * HALF);
+      if constexpr (MM) {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
+        for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[ks][i] = frag2<T, AKO>(ia, 16 * i, ks);
+          for (int i = 0; i < 4; ++i) fa[ks][i] = frag2<T, AKO>(ia, 16 * i, ks);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fb[ks][j] = frag2<T, BKO>(ib, bc + 16 * j, ks);
+          for (int j = 0; j < 2; ++j) fb[ks][j] = frag2<T, BKO>(ib, bc + 16 * j, ks);
+        }
       }
       pa0.issue(r + 2, anx);
-      quad(0, 0, fa, fb, acc);
+      quad(0, 0, fa, fb, acc, MM);
+      if constexpr (MM) {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+        for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int j = 2; j < 4; ++j) fb[ks][j] = frag2<T, BKO>(ib, bc + 16 * j, ks);
+          for (int j = 2; j < 4; ++j) fb[ks][j] = frag2<T, BKO>(ib, bc + 16 * j, ks);
+      }
       pa1.issue(r + 2, anx + HALF);
-      quad(0, 1, fa, fb, acc);
+      quad(0, 1, fa, fb, acc, MM);
+      if constexpr (MM) {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+        for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[ks][i] = frag2<T, AKO>(ia, 64 + 16 * i, ks);
-      quad(1, 1, fa, fb, acc);
+          for (int i = 0; i < 4; ++i) fa[ks][i] = frag2<T, AKO>(ia, 64 + 16 * i, ks);
+      }
+      quad(1, 1, fa, fb, acc, MM);
       pb0.issue(r + 2, bcur);
       pb1.issue(r + 2, bcur + HALF);
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -942,7 +955,7 @@ struct Loop8 {
         pb0.fix(r + 1, bnx);
         pb1.fix(r + 1, bnx + HALF);
       }
-      quad(1, 0, fa, fb, acc);
+      quad(1, 0, fa, fb, acc, MM);
       as = as == 2 ? 0 : as + 1;
     }
     if (!late) __builtin_amdgcn_s_barrier();  // re-align the two wave rows

@@ -18,6 +18,7 @@ Layout in HBM (per tower; row = b*T + t, dt = compute dtype):
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 from dataclasses import dataclass
 
@@ -336,6 +337,9 @@ def _gru_layer_bwd(cfg, layer, B, T, S, Y, dY, dfinal, packs):
     return dG, dbih, dbhh
 
 
+_WGRAD_T = os.environ.get("TT_WGRAD_T", "1") != "0"  # layer-0 dW_ih as its transpose (read once)
+
+
 def _weight_grads(cfg, B, T, dG, Xin, K, ldx, Y, kr=None):
     """dW_ih = dG^T Xin, dW_hh = dGH^T Y_{t-1} for all (tower, dir) in two batched TN GEMMs."""
     n, H, dt, dev = cfg.ntowers, cfg.H, cfg.dtype, dG[0].device
@@ -357,8 +361,19 @@ def _weight_grads(cfg, B, T, dG, Xin, K, ldx, Y, kr=None):
     kr = K if kr is None else kr  # layer 0: the real embedding columns, not the padding
     with timing.region("wgrad_ih", 1, 2.0 * 3 * H * kr * BT * 2 * n,
                        float(n * (esz * BT * (6 * H + kr) + 2 * 3 * H * kr * 4))):
-        ops.gemm(a_ih, b_ih, c_ih, m=3 * H, n=K, k=BT, lda=8 * H, ldb=ldx, ldc=K, a_kouter=True, b_kouter=True,
-                 dtype=dt, out_dtype=torch.float32)
+        if _WGRAD_T and dt == torch.bfloat16 and 0 < K % 256 <= 128:
+            # layer 0 (K = Ep 320): dW_ih^T = Xin^T dG puts the padded width on M, where the
+            # tail tile's second wave row lies wholly past M and skips its MFMAs (the
+            # 256x256 loop, tt_gemm_core.h Loop8::quad): 1.5 tiles of work per 256 gate
+            # rows instead of 2 for the N tail
+            cT = [_alloc((K, 3 * H), torch.float32, dev) for _ in c_ih]
+            ops.gemm(b_ih, a_ih, cT, m=K, n=3 * H, k=BT, lda=ldx, ldb=8 * H, ldc=3 * H, a_kouter=True,
+                     b_kouter=True, dtype=dt, out_dtype=torch.float32)
+            for c, ct in zip(c_ih, cT):
+                c.copy_(ct.t())
+        else:
+            ops.gemm(a_ih, b_ih, c_ih, m=3 * H, n=K, k=BT, lda=8 * H, ldb=ldx, ldc=K, a_kouter=True,
+                     b_kouter=True, dtype=dt, out_dtype=torch.float32)
     with timing.region("wgrad_hh", 1, 2.0 * 3 * H * H * BT * 2 * n,
                        float(n * (esz * BT * (6 * H + 2 * H) + 2 * 3 * H * H * 4))):
         ops.gemm(a_hh, b_hh, c_hh, m=3 * H, n=H, k=BT, lda=8 * H, ldb=2 * H, ldc=H, a_kouter=True, b_kouter=True,

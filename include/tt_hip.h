@@ -61,6 +61,19 @@ int tt_embed_gather(int dtype, const void* table, long vocab, int ep, const int3
  * reference's float [B,T,E] encoder input (enhanced_two_tower.py:50,56) into the
  * padded layout the projections read. */
 int tt_pack_rows(int dtype, const float* src, long n, int e, int ep, void* out, void* stream);
+/* Weight packing in one launch: up to 16 jobs, each dst[r][c] = src[r][c] (+ src2[r][c]) for
+ * c < cols and 0 for cols <= c < dcols, r < rows, written as bf16 (dst_bf16) or fp32. cols,
+ * dcols, lds, ldd multiples of 4 and src / src2 / dst 16-byte aligned. Replaces the per-step
+ * torch.cat / pad / cast of the GRU weights and the folded r|z biases (towers.py _Packed). */
+typedef struct {
+  const float* src;
+  const float* src2; /* NULL or a second fp32 operand of the same layout, added */
+  void* dst;
+  int rows, cols, dcols;
+  long lds, ldd;
+  int dst_bf16;
+} tt_pack_job;
+int tt_pack_multi(const tt_pack_job* jobs, int njobs, void* stream);
 
 /* y[i] = (dtype)x[i] (fp32 -> dtype) for n elements. */
 int tt_cast(int dtype, const float* x, long n, void* y, void* stream);

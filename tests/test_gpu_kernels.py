@@ -312,3 +312,29 @@ def test_gemm_tail_tile_idle_wave_row(m, akout, bkout):
     ref = A.float().to(DEV) @ B.float().to(DEV).t()
     assert not torch.isnan(C).any()
     assert rel_err(C, ref) < 1e-5, rel_err(C, ref)
+
+
+@pytest.mark.parametrize("E,hidden", [(300, 256), (16, 8), (300, 512)])
+def test_weight_pack_one_launch_matches_torch_pack(E, hidden):
+    """towers._Packed's bf16 path (tt_pack_multi: stacked W_ih with layer 0 zero-padded to
+    Ep, W_hh cast, r|z biases folded) against the torch path on the same parameters: every
+    packed tensor bit-identical."""
+    import two_towers_amd as tta
+    from two_towers_amd import towers
+    torch.manual_seed(E + hidden)
+    m = tta.EnhancedTwoTowerModel(E, hidden).to(DEV)
+    p = m._tower_params("query")
+    H = 2 * hidden
+    cfg = towers.TowerCfg(1, E, H, hidden, torch.bfloat16, 0.0)
+    Ep = ops.pad_cols(E, torch.bfloat16)
+    fast = towers._Packed(p, cfg, Ep)
+    ref = towers._Packed.__new__(towers._Packed)
+    ref.wih, ref.bias, ref.whh, ref.bhn = [], [], [], []
+    ref._pack_torch(dict(zip(towers.GRU_NAMES, p[:16])), H, E, Ep, torch.bfloat16)
+    torch.cuda.synchronize()
+    for layer in (0, 1):
+        assert torch.equal(fast.wih[layer], ref.wih[layer]), layer
+        assert torch.equal(fast.bias[layer], ref.bias[layer]), layer
+        for d in range(2):
+            assert torch.equal(fast.whh[layer][d], ref.whh[layer][d]), (layer, d)
+            assert torch.equal(fast.bhn[layer][d], ref.bhn[layer][d]), (layer, d)

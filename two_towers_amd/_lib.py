@@ -42,6 +42,20 @@ class GemmBatch(ctypes.Structure):
     ]
 
 
+class PackJob(ctypes.Structure):  # include/tt_hip.h tt_pack_job
+    _fields_ = [
+        ("src", c_void_p),
+        ("src2", c_void_p),
+        ("dst", c_void_p),
+        ("rows", c_int),
+        ("cols", c_int),
+        ("dcols", c_int),
+        ("lds", c_long),
+        ("ldd", c_long),
+        ("dst_bf16", c_int),
+    ]
+
+
 class GruFwdRec(ctypes.Structure):
     _fields_ = [
         ("g", c_void_p), ("whh", c_void_p), ("bhn", c_void_p), ("y", c_void_p), ("x1", c_void_p),
@@ -98,6 +112,7 @@ _SIGS = {
     "tt_get_option": (c_int, [ctypes.c_char_p, POINTER(c_int)]),
     "tt_embed_gather": (c_int, [c_int, c_void_p, c_long, c_int, c_void_p, c_long, c_void_p, c_void_p]),
     "tt_pack_rows": (c_int, [c_int, c_void_p, c_long, c_int, c_int, c_void_p, c_void_p]),
+    "tt_pack_multi": (c_int, [c_void_p, c_int, c_void_p]),
     "tt_cast": (c_int, [c_int, c_void_p, c_long, c_void_p, c_void_p]),
     "tt_colsum": (c_int, [c_void_p, c_long, c_int, c_long, c_void_p, c_int, c_void_p]),
     "tt_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, POINTER(GemmBatch), c_int, c_long,

@@ -71,6 +71,39 @@ __global__ __launch_bounds__(256) void sum_kernel(const float* __restrict__ x, l
   if (threadIdx.x == 0) out[0] = scale * (part[0] + part[1] + part[2] + part[3]);
 }
 
+struct PackArgs {
+  tt_pack_job j[16];
+  long start[17];  // prefix sums of rows * dcols / 4 (4-element groups per job)
+  int n;
+};
+__global__ __launch_bounds__(256) void pack_multi_kernel(PackArgs a) {
+  const long total = a.start[a.n];
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    int k = 0;
+    while (k + 1 < a.n && i >= a.start[k + 1]) ++k;
+    const tt_pack_job& J = a.j[k];
+    const long q = i - a.start[k];
+    const int g4 = J.dcols / 4;
+    const long r = q / g4;
+    const int c = (int)(q - r * g4) * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < J.cols) {
+      v = *reinterpret_cast<const float4*>(J.src + r * J.lds + c);
+      if (J.src2) {
+        const float4 w = *reinterpret_cast<const float4*>(J.src2 + r * J.lds + c);
+        v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+      }
+    }
+    if (J.dst_bf16) {
+      const uint2 o = make_uint2((uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16),
+                                 (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16));
+      *reinterpret_cast<uint2*>(static_cast<bf16_t*>(J.dst) + r * J.ldd + c) = o;
+    } else {
+      *reinterpret_cast<float4*>(static_cast<float*>(J.dst) + r * J.ldd + c) = v;
+    }
+  }
+}
+
 inline unsigned grid_for(long work, int per_block = 256, int cap = 8192) {
   long g = (work + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -101,6 +134,28 @@ extern "C" int tt_pack_rows(int dtype, const float* src, long n, int e, int ep, 
   else
     hipLaunchKernelGGL(pack_rows_kernel<float>, g, dim3(256), 0, (hipStream_t)stream, src, n, e, ep, (float*)out);
   TT_CHECK_LAUNCH("pack_rows_kernel");
+  return 0;
+}
+
+extern "C" int tt_pack_multi(const tt_pack_job* jobs, int njobs, void* stream) {
+  TT_CHECK_ARG(njobs >= 0 && njobs <= 16 && (njobs == 0 || jobs), "tt_pack_multi: njobs %d not in [0,16]", njobs);
+  PackArgs a{};
+  a.n = njobs;
+  a.start[0] = 0;
+  for (int k = 0; k < njobs; ++k) {
+    const tt_pack_job& J = jobs[k];
+    TT_CHECK_ARG(J.src && J.dst && J.rows >= 0 && J.cols >= 0 && J.dcols >= J.cols, "tt_pack_multi: job %d", k);
+    TT_CHECK_ARG(J.cols % 4 == 0 && J.dcols % 4 == 0 && J.lds % 4 == 0 && J.ldd % 4 == 0 && J.lds >= J.cols &&
+                     J.ldd >= J.dcols,
+                 "tt_pack_multi: job %d: cols, dcols and leading dimensions must be multiples of 4", k);
+    const bool src_ok = ((uintptr_t)J.src | (uintptr_t)J.src2) % 16 == 0;
+    TT_CHECK_ARG(src_ok && (uintptr_t)J.dst % (J.dst_bf16 ? 8 : 16) == 0, "tt_pack_multi: job %d: misaligned operand", k);
+    a.j[k] = J;
+    a.start[k + 1] = a.start[k] + (long)J.rows * (J.dcols / 4);
+  }
+  if (a.start[njobs] == 0) return 0;
+  hipLaunchKernelGGL(pack_multi_kernel, dim3(grid_for(a.start[njobs], 256, 4096)), dim3(256), 0, (hipStream_t)stream, a);
+  TT_CHECK_LAUNCH("pack_multi_kernel");
   return 0;
 }
 

@@ -62,6 +62,9 @@ class TowerCfg:
         return PARAMS_PER_TOWER if self.head == "proj2" else len(GRU_NAMES)
 
 
+_PACK_ONE = os.environ.get("TT_PACK_TORCH", "0") == "0"  # 0: bf16 packs in one launch (read once)
+
+
 class _Packed:
     """Per-step compute-dtype copies of one tower's weights in the kernels' layouts."""
 
@@ -73,6 +76,57 @@ class _Packed:
         self.bias = []
         self.whh = []
         self.bhn = []
+        if _PACK_ONE and dt == torch.bfloat16 and E % 4 == 0 and H % 4 == 0 and all(
+                t.is_contiguous() and t.dtype == torch.float32 and t.data_ptr() % 16 == 0 for t in p[:16]):
+            self._pack_bf16(g, H, E, Ep, p[0].device)
+        else:
+            self._pack_torch(g, H, E, Ep, dt)
+        if cfg.head == "none":
+            return
+        # The projection head always runs in fp32 (HEAD_DT): it is <1% of the FLOPs, and its
+        # backward is where the batch-wide cancellation of the contrastive-loss gradient
+        # would otherwise lose most of its precision to a bf16 cast.
+        self.w1 = hd["0.weight"].float().contiguous()
+        self.b1 = hd["0.bias"].float().contiguous()
+        self.ln_g = hd["1.weight"].float().contiguous()
+        self.ln_b = hd["1.bias"].float().contiguous()
+        self.w2 = hd["3.weight"].float().contiguous()
+        self.b2 = hd["3.bias"].float().contiguous()
+
+    def _pack_bf16(self, g, H, E, Ep, dev):
+        """The bf16 packs in one launch (tt_pack_multi): W_ih of both directions stacked
+        (layer 0 zero-padded to Ep columns), W_hh cast, biases with the r|z parts of b_hh
+        folded in -- the same values as _pack_torch (fp32 adds, round-to-nearest-even)."""
+        jobs = (_lib.PackJob * 16)()
+        nj = 0
+
+        def job(src, dst, rows, cols, dcols, lds, ldd, bf16, src2=None):
+            nonlocal nj
+            j = jobs[nj]
+            j.src, j.src2, j.dst = src, src2, dst
+            j.rows, j.cols, j.dcols, j.lds, j.ldd, j.dst_bf16 = rows, cols, dcols, lds, ldd, int(bf16)
+            nj += 1
+        for layer in (0, 1):
+            K = E if layer == 0 else 2 * H
+            Kp = Ep if layer == 0 else K
+            w = _alloc((6 * H, Kp), torch.bfloat16, dev)
+            b = _alloc((6 * H,), torch.float32, dev)
+            whh = []
+            for d, sfx in enumerate(("", "_reverse")):
+                job(g[f"weight_ih_l{layer}{sfx}"].data_ptr(), w.data_ptr() + d * 3 * H * Kp * 2, 3 * H, K, Kp, K, Kp, True)
+                bi, bh = g[f"bias_ih_l{layer}{sfx}"], g[f"bias_hh_l{layer}{sfx}"]
+                job(bi.data_ptr(), b.data_ptr() + d * 3 * H * 4, 1, 2 * H, 2 * H, 2 * H, 2 * H, False, bh.data_ptr())
+                job(bi.data_ptr() + 2 * H * 4, b.data_ptr() + (d * 3 + 2) * H * 4, 1, H, H, H, H, False)
+                wh = _alloc((3 * H, H), torch.bfloat16, dev)
+                job(g[f"weight_hh_l{layer}{sfx}"].data_ptr(), wh.data_ptr(), 3 * H, H, H, H, H, True)
+                whh.append(wh)
+            self.wih.append(w)
+            self.bias.append(b)
+            self.whh.append(whh)
+            self.bhn.append([g[f"bias_hh_l{layer}{s}"][2 * H:] for s in ("", "_reverse")])
+        call("tt_pack_multi", jobs, nj, stream_ptr(dev))
+
+    def _pack_torch(self, g, H, E, Ep, dt):
         for layer in (0, 1):
             wf, wr = g[f"weight_ih_l{layer}"], g[f"weight_ih_l{layer}_reverse"]
             w = torch.cat([wf, wr], 0)
@@ -86,17 +140,6 @@ class _Packed:
             self.bias.append(torch.cat(bs).float().contiguous())
             self.whh.append([g[f"weight_hh_l{layer}{s}"].to(dt).contiguous() for s in ("", "_reverse")])
             self.bhn.append([g[f"bias_hh_l{layer}{s}"][2 * H:].float().contiguous() for s in ("", "_reverse")])
-        if cfg.head == "none":
-            return
-        # The projection head always runs in fp32 (HEAD_DT): it is <1% of the FLOPs, and its
-        # backward is where the batch-wide cancellation of the contrastive-loss gradient
-        # would otherwise lose most of its precision to a bf16 cast.
-        self.w1 = hd["0.weight"].float().contiguous()
-        self.b1 = hd["0.bias"].float().contiguous()
-        self.ln_g = hd["1.weight"].float().contiguous()
-        self.ln_b = hd["1.bias"].float().contiguous()
-        self.w2 = hd["3.weight"].float().contiguous()
-        self.b2 = hd["3.bias"].float().contiguous()
 
 
 def _packed(p, cfg: TowerCfg, Ep: int, cache_ok: bool) -> _Packed:

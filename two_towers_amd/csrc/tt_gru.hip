@@ -681,6 +681,12 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
   constexpr bool CREG = TT_BWD_CREG != 0 && C::NP == 1;
   constexpr int NIT = 128 / C::RPI;  // epilogue row iterations per thread
   static_assert(!CREG || 128 * C::LDB * 2 + C::RPI * C::HP * 4 <= C::LDS, "carry image + one bias row of partials");
+  static_assert(!CREG || C::HP <= 512, "one bias column per thread");
+  // CREG: the workgroup's bias partials (4 gate rows x HP units, one column per thread) run
+  // in registers across the steps and are stored once at the end -- the same fp32 additions
+  // in the same order as a per-step read-modify-write of the (zeroed) partial row, without
+  // its exposed load latency in every step's reduction
+  float pacc[4] = {0.f, 0.f, 0.f, 0.f};
   for (int s = T_ - 1; s >= 0; --s) {
     const int t = R.dir ? T_ - 1 - s : s;
     const int tn = R.dir ? t - 1 : t + 1;
@@ -938,11 +944,11 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) red[rsub * C::HP + jg + e] = bsum[q][e];
         __syncthreads();
-        for (int c = tid; c < C::HP; c += 512) {
+        if (tid < C::HP) {
           float v = 0.f;
 #pragma unroll
-          for (int w = 0; w < C::RPI; ++w) v += red[w * C::HP + c];
-          part[q * H + u0 + c] += v;
+          for (int w = 0; w < C::RPI; ++w) v += red[w * C::HP + tid];
+          pacc[q] += v;
         }
         __syncthreads();
       }
@@ -969,6 +975,11 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
 #pragma unroll 1
       for (int pass = 0; pass < C::NP; ++pass) column_pass(pass * C::HP);
     }
+  }
+  if constexpr (CREG) {
+    if (tid < C::HP)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) part[q * H + tid] = pacc[q];
   }
 }
 

@@ -682,11 +682,14 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
   constexpr int NIT = 128 / C::RPI;  // epilogue row iterations per thread
   static_assert(!CREG || 128 * C::LDB * 2 + C::RPI * C::HP * 4 <= C::LDS, "carry image + one bias row of partials");
   static_assert(!CREG || C::HP <= 512, "one bias column per thread");
-  // CREG: the workgroup's bias partials (4 gate rows x HP units, one column per thread) run
-  // in registers across the steps and are stored once at the end -- the same fp32 additions
-  // in the same order as a per-step read-modify-write of the (zeroed) partial row, without
-  // its exposed load latency in every step's reduction
-  float pacc[4] = {0.f, 0.f, 0.f, 0.f};
+  // CREG: every thread's bias sums (4 gates x its 8 units) run over all its rows of all
+  // steps in registers, and the workgroup reduces them across its 8 row groups once, at the
+  // end (a per-step reduction cost 8 barriers and an LDS round trip per step)
+  float bacc[4][8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bacc[q][e] = 0.f;
   for (int s = T_ - 1; s >= 0; --s) {
     const int t = R.dir ? T_ - 1 - s : s;
     const int tn = R.dir ? t - 1 : t + 1;
@@ -865,11 +868,14 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
                                   wc * (C::HP / 4) + 16 * jc + 4 * (lane >> 4)) = make_uint2(w0, w1);
       }
     __syncthreads();
-    float bsum[4][8];
+    float bsum_own[4][8];
+    auto& bsum = CREG ? bacc : bsum_own;
+    if constexpr (!CREG) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) bsum[q][e] = 0.f;
+        for (int e = 0; e < 8; ++e) bsum[q][e] = 0.f;
+    }
     constexpr int NB = TT_BWD_NB;  // rows per batch of epilogue loads
     auto batch = [&](const int kb) {
       uint4 vin[NB][7];
@@ -935,24 +941,8 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
     };
 #pragma unroll 1
     for (int kb = 0; kb < NIT; kb += NB) batch(kb);
-    __syncthreads();
-    if constexpr (CREG) {
-      // the bias partials one gate row at a time, past the carry image
-      float* red = reinterpret_cast<float*>(lds + 128 * C::LDB * 2);
-#pragma unroll 1
-      for (int q = 0; q < 4; ++q) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) red[rsub * C::HP + jg + e] = bsum[q][e];
-        __syncthreads();
-        if (tid < C::HP) {
-          float v = 0.f;
-#pragma unroll
-          for (int w = 0; w < C::RPI; ++w) v += red[w * C::HP + tid];
-          pacc[q] += v;
-        }
-        __syncthreads();
-      }
-    } else {
+    if constexpr (!CREG) {  // (CREG: the step-end barrier below orders the carry image)
+      __syncthreads();
       float* red = L;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -977,9 +967,21 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
     }
   }
   if constexpr (CREG) {
-    if (tid < C::HP)
+    // the bias partials one gate row at a time (the LDS is free after the last step)
+    float* red = reinterpret_cast<float*>(lds);
+#pragma unroll 1
+    for (int q = 0; q < 4; ++q) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) part[q * H + tid] = pacc[q];
+      for (int e = 0; e < 8; ++e) red[rsub * C::HP + jg + e] = bacc[q][e];
+      __syncthreads();
+      if (tid < C::HP) {
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < C::RPI; ++w) v += red[w * C::HP + tid];
+        part[q * H + tid] = v;
+      }
+      __syncthreads();
+    }
   }
 }
 

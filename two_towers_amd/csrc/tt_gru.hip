@@ -379,6 +379,9 @@ TT_DEV void unpack8(uint4 v, float (&f)[8]) {
 #ifndef TT_BWD_NT
 #define TT_BWD_NT 3
 #endif
+#ifndef TT_BWD_PIPE  // gru_bwd_rows epilogue: 1 rows one ahead (loads before the previous row's stores); 0 batches of NB
+#define TT_BWD_PIPE 1
+#endif
 #ifndef TT_BWD_CREG  // gru_bwd_rows: the BPTT carry in registers (0: bf16 ping-pong buffer in HBM)
 #define TT_BWD_CREG 1
 #endif
@@ -877,70 +880,89 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
         for (int e = 0; e < 8; ++e) bsum[q][e] = 0.f;
     }
     constexpr int NB = TT_BWD_NB;  // rows per batch of epilogue loads
+    // one epilogue row of this thread (row rsub + RPI k of the tile): its 7 operand loads ...
+    auto load_row = [&](const int k, uint4 (&v)[7]) {
+      const int bl = rsub + C::RPI * k;
+      const bool ok = m0 + bl < a.B && !(dbg & 2);
+      const uint32_t oc = ok ? (uint32_t)(bl * H + u0 + jg) * 2u : 0x80000000u;
+      const uint32_t oy = ok ? (uint32_t)(bl * T_ * (int)a.ldy + u0 + jg) * 2u : 0x80000000u;
+      const uint32_t os = ok ? (uint32_t)(bl * T_ * 4 * H + u0 + jg) * 2u : 0x80000000u;
+      v[0] = CREG ? make_uint4(0, 0, 0, 0) : ld16_buf(rc, oc, 0);  // CREG: the carry is in gm
+      // TT_BWD_NT: non-temporal loads of the once-read streams (1: S, 2: dy and h_{s-1}), so
+      // that they do not displace the re-read gate gradients from the caches
+      v[1] = ld16_buf<(TT_BWD_NT & 2) ? 2 : 0>(rd, oy, 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[2 + q] = ld16_buf<(TT_BWD_NT & 1) ? 2 : 0>(rsv, os, q * 2 * H);
+      v[6] = ld16_buf<(TT_BWD_NT & 2) ? 2 : 0>(ry, oy, 0);
+    };
+    // ... and its gate math, carry and stores
+    auto finish_row = [&](const int k, const uint4 (&v)[7]) {
+      const int bl = rsub + C::RPI * k;
+      const int b = m0 + bl;
+      if (b >= a.B) return;
+      float cin[8], dy[8], ar[8], az[8], an[8], gh[8], hp[8], gm[8];
+      unpack8(v[0], cin);
+      unpack8(v[1], dy);
+      unpack8(v[2], ar);
+      unpack8(v[3], az);
+      unpack8(v[4], an);
+      unpack8(v[5], gh);
+      unpack8(v[6], hp);
+      unpack8(*reinterpret_cast<const uint4*>(L16 + ((bl * C::LDB + jg) >> 1)), gm);
+      if (last && R.dfinal) ld8(R.dfinal + (long)b * a.ldf + u0 + jg, cin);
+      float o_r[8], o_z[8], o_n[8], o_hn[8], cout[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float dht = gm[e] + cin[e] + dy[e];
+        float rg, omr, zg, omz, ng, sech2;
+        tt_sigmoid_pair(ar[e], rg, omr);
+        tt_sigmoid_pair(az[e], zg, omz);
+        tt_tanh_sech2(an[e], ng, sech2);
+        const float dnp = dht * omz * sech2;
+        const float drp = dnp * gh[e] * rg * omr;
+        const float dzp = dht * (hp[e] - ng) * zg * omz;
+        o_r[e] = drp; o_z[e] = dzp; o_n[e] = dnp; o_hn[e] = dnp * rg;
+        cout[e] = dht * zg;
+        bsum[0][e] += drp; bsum[1][e] += dzp; bsum[2][e] += dnp; bsum[3][e] += dnp * rg;
+      }
+      if constexpr (CREG)  // over the gm slot this thread just read: the next step's carry
+        *reinterpret_cast<uint4*>(L16 + ((bl * C::LDB + jg) >> 1)) = pack8bf(cout);
+      if (dbg & 4) {
+        if (o_r[0] == 12345.f) L16[0] = __float_as_uint(o_z[1] + o_n[2] + o_hn[3] + cout[4]);
+        return;
+      }
+      if constexpr (!CREG) st8(cr_cur + (long)bl * H + u0 + jg, cout);
+      const long row = (long)b * T_ + t;
+      bf16_t* xw = DGXw + row * a.ldd + u0 + jg;
+      st8(xw, o_r);
+      st8(xw + H, o_z);
+      st8_sc1(grs, (int)(((long)bl * T_ * a.ldd + u0 + jg + 2 * H) * 2L), o_n, (bf16_t*)nullptr);
+      st8(DGHw + row * a.ldd + u0 + jg, o_hn);
+    };
     auto batch = [&](const int kb) {
       uint4 vin[NB][7];
 #pragma unroll
-      for (int kk = 0; kk < NB; ++kk) {
-        const int bl = rsub + C::RPI * (kb + kk);
-        const bool ok = m0 + bl < a.B && !(dbg & 2);
-        const uint32_t oc = ok ? (uint32_t)(bl * H + u0 + jg) * 2u : 0x80000000u;
-        const uint32_t oy = ok ? (uint32_t)(bl * T_ * (int)a.ldy + u0 + jg) * 2u : 0x80000000u;
-        const uint32_t os = ok ? (uint32_t)(bl * T_ * 4 * H + u0 + jg) * 2u : 0x80000000u;
-        vin[kk][0] = CREG ? make_uint4(0, 0, 0, 0) : ld16_buf(rc, oc, 0);  // CREG: the carry is in gm
-        // TT_BWD_NT: non-temporal loads of the once-read streams (1: S, 2: dy and h_{s-1}), so
-        // that they do not displace the re-read gate gradients from the caches
-        vin[kk][1] = ld16_buf<(TT_BWD_NT & 2) ? 2 : 0>(rd, oy, 0);
+      for (int kk = 0; kk < NB; ++kk) load_row(kb + kk, vin[kk]);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) vin[kk][2 + q] = ld16_buf<(TT_BWD_NT & 1) ? 2 : 0>(rsv, os, q * 2 * H);
-        vin[kk][6] = ld16_buf<(TT_BWD_NT & 2) ? 2 : 0>(ry, oy, 0);
-      }
-#pragma unroll
-      for (int kk = 0; kk < NB; ++kk) {
-        const int bl = rsub + C::RPI * (kb + kk);
-        const int b = m0 + bl;
-        if (b >= a.B) continue;
-        float cin[8], dy[8], ar[8], az[8], an[8], gh[8], hp[8], gm[8];
-        unpack8(vin[kk][0], cin);
-        unpack8(vin[kk][1], dy);
-        unpack8(vin[kk][2], ar);
-        unpack8(vin[kk][3], az);
-        unpack8(vin[kk][4], an);
-        unpack8(vin[kk][5], gh);
-        unpack8(vin[kk][6], hp);
-        unpack8(*reinterpret_cast<const uint4*>(L16 + ((bl * C::LDB + jg) >> 1)), gm);
-        if (last && R.dfinal) ld8(R.dfinal + (long)b * a.ldf + u0 + jg, cin);
-        float o_r[8], o_z[8], o_n[8], o_hn[8], cout[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float dht = gm[e] + cin[e] + dy[e];
-          float rg, omr, zg, omz, ng, sech2;
-          tt_sigmoid_pair(ar[e], rg, omr);
-          tt_sigmoid_pair(az[e], zg, omz);
-          tt_tanh_sech2(an[e], ng, sech2);
-          const float dnp = dht * omz * sech2;
-          const float drp = dnp * gh[e] * rg * omr;
-          const float dzp = dht * (hp[e] - ng) * zg * omz;
-          o_r[e] = drp; o_z[e] = dzp; o_n[e] = dnp; o_hn[e] = dnp * rg;
-          cout[e] = dht * zg;
-          bsum[0][e] += drp; bsum[1][e] += dzp; bsum[2][e] += dnp; bsum[3][e] += dnp * rg;
-        }
-        if constexpr (CREG)  // over the gm slot this thread just read: the next step's carry
-          *reinterpret_cast<uint4*>(L16 + ((bl * C::LDB + jg) >> 1)) = pack8bf(cout);
-        if (dbg & 4) {
-          if (o_r[0] == 12345.f) L16[0] = __float_as_uint(o_z[1] + o_n[2] + o_hn[3] + cout[4]);
-          continue;
-        }
-        if constexpr (!CREG) st8(cr_cur + (long)bl * H + u0 + jg, cout);
-        const long row = (long)b * T_ + t;
-        bf16_t* xw = DGXw + row * a.ldd + u0 + jg;
-        st8(xw, o_r);
-        st8(xw + H, o_z);
-        st8_sc1(grs, (int)(((long)bl * T_ * a.ldd + u0 + jg + 2 * H) * 2L), o_n, (bf16_t*)nullptr);
-        st8(DGHw + row * a.ldd + u0 + jg, o_hn);
-      }
+      for (int kk = 0; kk < NB; ++kk) finish_row(kb + kk, vin[kk]);
     };
+#if TT_BWD_PIPE
+    // rows one ahead: row k+1's loads go out before row k's stores, so the wait for a row's
+    // loads never covers the stores of the row before it (one in-order vmcnt)
+    static_assert(NIT % 2 == 0, "rows in pairs");
+    uint4 vr[2][7];
+    load_row(0, vr[0]);
+#pragma unroll 1
+    for (int k = 0; k < NIT; k += 2) {
+      load_row(k + 1, vr[1]);
+      finish_row(k, vr[0]);
+      if (k + 2 < NIT) load_row(k + 2, vr[0]);
+      finish_row(k + 1, vr[1]);
+    }
+#else
 #pragma unroll 1
     for (int kb = 0; kb < NIT; kb += NB) batch(kb);
+#endif
     if constexpr (!CREG) {  // (CREG: the step-end barrier below orders the carry image)
       __syncthreads();
       float* red = L;

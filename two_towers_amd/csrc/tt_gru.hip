@@ -881,9 +881,9 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
     }
     constexpr int NB = TT_BWD_NB;  // rows per batch of epilogue loads
     // one epilogue row of this thread (row rsub + RPI k of the tile): its 7 operand loads ...
-    auto load_row = [&](const int k, uint4 (&v)[7]) {
+    auto load_row = [&](const int k, uint4 (&v)[7]) {  // k >= NIT: out of range, reads zero
       const int bl = rsub + C::RPI * k;
-      const bool ok = m0 + bl < a.B && !(dbg & 2);
+      const bool ok = k < NIT && m0 + bl < a.B && !(dbg & 2);
       const uint32_t oc = ok ? (uint32_t)(bl * H + u0 + jg) * 2u : 0x80000000u;
       const uint32_t oy = ok ? (uint32_t)(bl * T_ * (int)a.ldy + u0 + jg) * 2u : 0x80000000u;
       const uint32_t os = ok ? (uint32_t)(bl * T_ * 4 * H + u0 + jg) * 2u : 0x80000000u;
@@ -909,7 +909,22 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
       unpack8(v[5], gh);
       unpack8(v[6], hp);
       unpack8(*reinterpret_cast<const uint4*>(L16 + ((bl * C::LDB + jg) >> 1)), gm);
-      if (last && R.dfinal) ld8(R.dfinal + (long)b * a.ldf + u0 + jg, cin);
+      if (last && R.dfinal) {
+        // the fp32 final-state gradient (first step of the launch only), loaded and waited
+        // for inside one asm block: a compiler-visible conditional load here would put a
+        // vmcnt(0) on every row's path and drain the next row's loads (TT_BWD_PIPE)
+        const float* pf = R.dfinal + (long)b * a.ldf + u0 + jg;
+        tt_u32x4 d0, d1;
+        asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %2, off offset:16\n\ts_waitcnt vmcnt(0)"
+                     : "=&v"(d0), "=&v"(d1)
+                     : "v"(pf)
+                     : "memory");
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          cin[e] = __uint_as_float(d0[e]);
+          cin[4 + e] = __uint_as_float(d1[e]);
+        }
+      }
       float o_r[8], o_z[8], o_n[8], o_hn[8], cout[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -956,8 +971,8 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
     for (int k = 0; k < NIT; k += 2) {
       load_row(k + 1, vr[1]);
       finish_row(k, vr[0]);
-      if (k + 2 < NIT) load_row(k + 2, vr[0]);
-      finish_row(k + 1, vr[1]);
+      load_row(k + 2, vr[0]);  // unconditional (the last pair's is out of range): no branch whose
+      finish_row(k + 1, vr[1]);  // merge would make the next wait drain every load
     }
 #else
 #pragma unroll 1

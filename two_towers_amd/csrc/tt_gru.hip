@@ -1797,6 +1797,9 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
 // so each SIMD's matrix pipe and vector issue are fed by different waves (MI355X_MICROARCH.md
 // "Two waves per SIMD"), with ONE barrier per chunk. The MFMA sequence per chunk and the
 // cell are gru_fwd_xcp's (same k order from zero, gru_cell): bit-identical outputs.
+#ifndef XS_MPOLL  // gru_fwd_xs: the group counters polled by matrix wave 0 (0: by vector thread 0)
+#define XS_MPOLL 1
+#endif
 #ifndef XS_GA  // gru_fwd_xs: chunks of gate inputs requested ahead
 #define XS_GA 1
 #endif
@@ -1920,6 +1923,14 @@ __global__ __launch_bounds__(xs::NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2)
 #pragma unroll
       for (int c = 0; c < xc::NCH; ++c) {
         if (c + 1 < xc::NCH || has_next) chunk(slots + ((c + 1) & 1) * C::SLOT, stgb + ((c + 1) & 1) * (xc::STG / 4));
+#if XS_MPOLL
+        // the group counters are polled by a matrix-wave lane (its memory queue is empty, so a
+        // poll drains nothing; a vector-wave poll waited for that wave's stores)
+        if (tid == 0 && !(dbg & 32)) {
+          if (c == 0 && idx > 0) xc_wait(cntB, (unsigned)(M * idx), ws);
+          if (c == 4 && has_next) xc_wait(cntA, (unsigned)(M * (idx + 1)), ws);
+        }
+#endif
         __syncthreads();
       }
     }
@@ -2054,7 +2065,7 @@ __global__ __launch_bounds__(xs::NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2)
       }
       if (c + 3 < xc::NCH) load_h(cur, idx, c + 3);
       else if (has_next) load_h(nxt, idx + 1, c + 3 - xc::NCH);
-      if (vt == 0 && !(dbg & 32)) {
+      if (!XS_MPOLL && vt == 0 && !(dbg & 32)) {
         if (c == 0 && idx > 0) xc_wait(cntB, (unsigned)(M * idx), ws);
         if (c == 4 && has_next) xc_wait(cntA, (unsigned)(M * (idx + 1)), ws);
       }

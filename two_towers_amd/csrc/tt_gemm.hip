@@ -411,6 +411,9 @@ TT_DEV void epi_direct(const GemmArgs& g, const f32x4 (&acc)[8][4], TO* C, const
 #ifndef BRES_STORE  // output store policy of gemm_bres: 0 plain, 1 write-through (sc1), 2 non-temporal
 #define BRES_STORE 0
 #endif
+#ifndef BRES_PD  // gemm_bres A prefetch: 1 a whole tile ahead, 0 half a tile
+#define BRES_PD 1
+#endif
 #ifndef BRES_STAG  // waves 4-7 start BRES_STAG x 64 cycles late (0: together)
 #define BRES_STAG 0
 #endif
@@ -419,7 +422,9 @@ template <int NKS>  // k-steps of 32
 __global__ __launch_bounds__(512, 1) void gemm_bres(GemmArgs g, int npan, int nbatch) {
   constexpr int NKT = (NKS + 1) / 2;  // 64-deep K-tile images
   constexpr int IMG = BR_COLS * ttg::KTB;
-  constexpr int PD = NKS % 2 == 0 ? NKS / 2 : NKS;  // A prefetch depth in k-steps (divides NKS)
+  // A prefetch depth in k-steps (divides NKS); BRES_PD 1: a whole tile, so that the next
+  // tile's fragments are all requested before this tile's stores (one in-order vmcnt)
+  constexpr int PD = ((BRES_PD && NKS <= 10) || NKS % 2 != 0) ? NKS : NKS / 2;  // (NKS 12: 20 spills)
   __shared__ __attribute__((aligned(16))) char lds[NKT * IMG + BR_COLS * 4];
   float* bias_s = reinterpret_cast<float*>(lds + NKT * IMG);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;

@@ -1797,6 +1797,9 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
 // so each SIMD's matrix pipe and vector issue are fed by different waves (MI355X_MICROARCH.md
 // "Two waves per SIMD"), with ONE barrier per chunk. The MFMA sequence per chunk and the
 // cell are gru_fwd_xcp's (same k order from zero, gru_cell): bit-identical outputs.
+#ifndef XS_MPUB  // gru_fwd_xs: arrivals published by matrix wave 0 (0: by vector thread 0)
+#define XS_MPUB 1
+#endif
 #ifndef XS_MPOLL  // gru_fwd_xs: the group counters polled by matrix wave 0 (0: by vector thread 0)
 #define XS_MPOLL 1
 #endif
@@ -1932,6 +1935,12 @@ __global__ __launch_bounds__(xs::NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2)
         }
 #endif
         __syncthreads();
+#if XS_MPUB
+        // ... and the arrivals published by it too, after the barrier that follows every vector
+        // wave's drain of its exchange stores (keeps the atomic out of a storing wave's queue)
+        if (tid == 0 && c == 3 && publish) __hip_atomic_fetch_add(cntA, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0 && c == 7 && publish) __hip_atomic_fetch_add(cntB, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
       }
     }
     return;
@@ -2070,8 +2079,8 @@ __global__ __launch_bounds__(xs::NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2)
         if (c == 4 && has_next) xc_wait(cntA, (unsigned)(M * (idx + 1)), ws);
       }
       __syncthreads();
-      if (vt == 0 && c == 3 && publish) __hip_atomic_fetch_add(cntA, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (vt == 0 && c == 7 && publish) __hip_atomic_fetch_add(cntB, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!XS_MPUB && vt == 0 && c == 3 && publish) __hip_atomic_fetch_add(cntA, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!XS_MPUB && vt == 0 && c == 7 && publish) __hip_atomic_fetch_add(cntB, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     cur = nxt;
     rGc = rGn;

@@ -40,11 +40,13 @@ const char* tt_version(void);
 const char* tt_last_error(void);
 /* Kernel-variant switches (process-wide; initialised once from the environment variable
  * of the same name in upper case with a TT_ prefix, e.g. gru_step <- TT_GRU_STEP):
- * gru_step, gru_depth, gru_bwd_rows, gru_bwd_big, gru_bwd_streams, gru_bwd_persist,
- * gru_fwd_step_rows, gru_fwd_xc, gemm_persist, gemm_a3, gemm_regstage, gemm_stream_out,
- * gemm_skew, gemm_persist_maxk, hn_gemm, hn_map, infonce_flash; diagnostics gru_xc_skip,
- * gru_xc_spins. Every variant computes the same function; they exist for A/B measurement
- * and for tests that compare variants.
+ * GRU: gru_step, gru_depth, gru_bwd_rows, gru_bwd_big, gru_bwd_streams, gru_bwd_persist,
+ * gru_bwd_skew, gru_fwd_step_rows, gru_fwd_xc, gru_fwd_xs, gru_fwd_skew, gru_xc_coop,
+ * gru_step_ring; GEMM: gemm_persist, gemm_persist_maxk, gemm_a3, gemm_buf, gemm_bres,
+ * gemm_order, gemm_skew, gemm_regstage, gemm_stream_out; losses: hn_gemm, hn_map,
+ * infonce_flash; diagnostics gru_xc_skip, gru_xc_spins. The authoritative list with
+ * defaults is kOpts in two_towers_amd/csrc/tt_gemm.hip. Every variant computes the same
+ * function; they exist for A/B measurement and for tests that compare variants.
  * Not synchronised with launches in flight: set them between steps. */
 int tt_set_option(const char* name, int value);
 int tt_get_option(const char* name, int* value);
@@ -95,12 +97,8 @@ int tt_colsum(const float* x, long rows, int cols, long ld, float* out, int accu
  * (tt_gemm_ws_size floats) and are reduced into C; relu/dropout unsupported then.
  * out_dtype is TT_DT_F32 or dtype. Any m, n, k; operand base pointers and leading
  * dimensions must be 16-byte aligned (lda * sizeof(dtype) % 16 == 0).
- * Library path (option gemm_lt, default 1): a one-split bf16 -> bf16 problem with both
- * operands K-contiguous, alpha 1, no accumulate / relu / dropout / shift / a_split,
- * k >= 512 and m >= 65536 (the layer-1 input projection) runs on hipBLASLt when the caller
- * passes splitk_ws with tt_gemm_ws_size(m, n, nbatch, 1) floats (TT_GEMM_LT_WS bytes);
- * with splitk_ws NULL it runs on the hand-written kernels. */
-#define TT_GEMM_LT_WS (64L << 20)
+ * Every problem runs on the hand-written MFMA kernels of this library (tt_gemm.hip,
+ * tt_gemm_core.h); no vendor GEMM is linked. */
 typedef struct {
   const void* a[4];
   const void* b[4];
@@ -120,8 +118,7 @@ int tt_gemm(int dtype, int out_dtype, int a_kouter, int b_kouter, int m, int n, 
             const tt_gemm_batch* batch, int nbatch, long lda, long ldb, long ldc, float alpha,
             int beta_accum, int relu, int seq_t, uint32_t drop_seed, float drop_p, int splits,
             float* splitk_ws, void* stream);
-/* fp32 elements of splitk_ws: the split partials for splits > 1; for splits = 1 the
- * library path's workspace (TT_GEMM_LT_WS bytes) when m >= 65536, else 0. */
+/* fp32 elements of splitk_ws: the split partials for splits > 1, else 0. */
 long tt_gemm_ws_size(int m, int n, int nbatch, int splits);
 /* Heuristic split count for a (m, n, k, nbatch) problem. */
 int tt_gemm_pick_splits(int m, int n, int k, int nbatch);

@@ -90,6 +90,18 @@ def test_library_exports_every_header_symbol():
     assert lib.tt_version().decode().startswith("tt_hip")
 
 
+def test_library_links_no_vendor_math_library():
+    """Every kernel on the path is hand-written (north star: no dual backends): the shared
+    library's dynamic dependencies name no vendor BLAS / DNN / GEMM library."""
+    import subprocess
+    from two_towers_amd import _lib
+    out = subprocess.run(["readelf", "-d", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    needed = [ln.split("[")[1].rstrip("]") for ln in out.splitlines() if "(NEEDED)" in ln]
+    assert needed, out
+    vendor = [n for n in needed if any(v in n for v in ("blas", "MIOpen", "miopen", "rocsparse", "hipsparse", "ck_"))]
+    assert not vendor, needed
+
+
 def test_library_has_no_unprotected_wide_buffer_stores():
     """No 16/12-byte buffer store in the built gfx950 code takes its soffset from a
     register: LLVM inserts no wait states for that form, and a VALU write of the store's
@@ -170,9 +182,8 @@ def test_split_k_picker_fills_the_chip():
         assert s > 1, (m, n, k, s)
         assert k // s >= 64 * 8 or s == 1
     assert lib.tt_gemm_pick_splits(524288, 3072, 1024, 2) == 1
-    # one-split calls: the library path's workspace (TT_GEMM_LT_WS = 64 MiB) from M 65536 on
-    assert lib.tt_gemm_ws_size(524288, 3072, 2, 1) == (64 << 20) // 4
-    assert lib.tt_gemm_ws_size(65535, 3072, 2, 1) == 0
+    # one-split calls need no workspace (no library path: every GEMM is hand-written)
+    assert lib.tt_gemm_ws_size(524288, 3072, 2, 1) == 0
     assert lib.tt_gemm_ws_size(1536, 1024, 4, 8) == 1536 * 1024 * 4 * 8
     assert lib.tt_gru_fwd_launches(1, 64, 512) == 1 and lib.tt_gru_fwd_launches(0, 64, 512) == 64
 

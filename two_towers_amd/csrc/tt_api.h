@@ -42,13 +42,9 @@ enum Opt {
   OPT_GEMM_ORDER,       // 1: persistent GEMM tiles in column groups per XCD
   OPT_GRU_STEP_RING,    // LDS stages of the per-step GRU kernels' product (2: double buffer; fwd uses <= 3)
   OPT_GRU_FWD_XS,       // 1: column-split forward with matrix and vector waves (gru_fwd_xs, H 512); 0: gru_fwd_xcp
-  OPT_GEMM_LT,          // 1: the plain bf16 input projection (K >= 512) through hipBLASLt (tt_gemm_lt.hip)
   OPT_N
 };
 int opt(Opt o);
-// tt_gemm_lt.hip: C_b = A_b B_b^T (+ bias_b), bf16, both operands K-contiguous; ws: TT_GEMM_LT_WS bytes
-int gemm_lt(int m, int n, int k, const void* const* a, const void* const* b, void* const* c,
-            const float* const* bias, int nbatch, long lda, long ldb, long ldc, void* ws, hipStream_t st);
 }  // namespace tt
 
 #define TT_CHECK_ARG(cond, ...)            \

@@ -40,7 +40,7 @@ constexpr OptDef kOpts[OPT_N] = {
     {"gru_fwd_skew", "TT_GRU_FWD_SKEW", 0},       {"gemm_bres", "TT_GEMM_BRES", 1},
     {"gru_xc_coop", "TT_GRU_XC_COOP", 0},         {"gemm_buf", "TT_GEMM_BUF", 1},
     {"gemm_order", "TT_GEMM_ORDER", 0},           {"gru_step_ring", "TT_GRU_STEP_RING", 4},
-    {"gru_fwd_xs", "TT_GRU_FWD_XS", 1},           {"gemm_lt", "TT_GEMM_LT", 1},
+    {"gru_fwd_xs", "TT_GRU_FWD_XS", 1},
 };
 struct OptTable {
   std::atomic<int> v[OPT_N];
@@ -1016,8 +1016,8 @@ int launch_gemm(int akout, int bkout, bool shift, GemmArgs& g, int nbatch, hipSt
 }  // namespace
 
 extern "C" long tt_gemm_ws_size(int m, int n, int nbatch, int splits) {
-  if (splits > 1) return (long)m * n * nbatch * splits;
-  return m >= 65536 ? TT_GEMM_LT_WS / 4 : 0;
+  (void)m;
+  return splits > 1 ? (long)m * n * nbatch * splits : 0;
 }
 
 extern "C" int tt_gemm_pick_splits(int m, int n, int k, int nbatch) {
@@ -1125,11 +1125,6 @@ extern "C" int tt_gemm(int dtype, int out_dtype, int a_kouter, int b_kouter, int
       hipLaunchKernelGGL(splitk_reduce_kernel<bf16_t>, rg, dim3(256), 0, st, splitk_ws, gp.part_stride, splits, m, n, g);
     TT_CHECK_LAUNCH("splitk_reduce_kernel");
     return 0;
-  }
-  if (dtype == TT_DT_BF16 && out_dtype == TT_DT_BF16 && !a_kouter && !b_kouter && !shift && g.a_split == 0 &&
-      alpha == 1.f && !beta_accum && !relu && drop_p == 0.f && k >= 512 && m >= 65536 && splitk_ws &&
-      tt::opt(tt::OPT_GEMM_LT)) {  // library path (tt_gemm_lt.hip)
-    return tt::gemm_lt(m, n, k, g.a, g.b, g.c, g.bias, nbatch, lda, ldb, ldc, splitk_ws, st);
   }
   if (dtype == TT_DT_BF16) {
     return out_dtype == TT_DT_BF16 ? launch_gemm<bf16_t, bf16_t>(a_kouter, b_kouter, shift, g, nbatch, st)

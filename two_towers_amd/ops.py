@@ -59,11 +59,6 @@ def gemm(a: Sequence[torch.Tensor], b: Sequence[torch.Tensor], c: Sequence[torch
         ws = torch.empty(lib.tt_gemm_ws_size(m, n, nb, splits), dtype=torch.float32, device=c[0].device)
     else:
         splits = 1
-        if (dtype == torch.bfloat16 and out_dtype == torch.bfloat16 and not a_kouter and not b_kouter and k >= 512
-                and not (relu or drop_p or accumulate or a_split or any(bshift or ())) and alpha == 1.0):
-            nws = lib.tt_gemm_ws_size(m, n, nb, 1)  # the library path's workspace (include/tt_hip.h)
-            if nws > 0:
-                ws = torch.empty(nws, dtype=torch.float32, device=c[0].device)
     call("tt_gemm", dtype_code(dtype), dtype_code(out_dtype), int(a_kouter), int(b_kouter), m, n, k,
          ctypes.byref(bt), nb, lda, ldb, ldc, alpha, int(accumulate), int(relu), seq_t, drop_seed & 0xFFFFFFFF,
          drop_p, splits, ptr(ws), stream_ptr(c[0].device))

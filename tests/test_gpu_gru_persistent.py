@@ -222,6 +222,10 @@ def test_column_split_member_timeout_is_reported_and_not_sticky():
     opt.step()  # one healthy step, so the moments are non-zero
     opt.zero_grad()
     tta.check_gru_status()
+    # the guard the first timed-out forward armed was cleared once the host had been told of
+    # it (the raise above), so this step trained
+    for p in m.parameters():
+        assert opt.state[p]["exp_avg_sq"].abs().sum() > 0
     before = {k: v.detach().clone() for k, v in m.state_dict().items()}
     moments = {id(p): (opt.state[p]["exp_avg"].clone(), opt.state[p]["exp_avg_sq"].clone()) for p in m.parameters()}
     with option("gru_xc_spins", 14), option("gru_xc_skip", 1):
@@ -250,6 +254,20 @@ def test_column_split_member_timeout_is_reported_and_not_sticky():
     opt.step()
     tta.check_gru_status()
     assert any(not torch.equal(v, before[k]) for k, v in m.state_dict().items())
+    # the skipped step is not counted: two applied updates
+    opt.settle_skipped_steps()
+    assert all(int(opt.state[p]["step"]) == 2 for p in m.parameters())
+    # an eval / no-grad forward that times out does not arm the guard
+    with torch.no_grad(), option("gru_xc_spins", 14), option("gru_xc_skip", 1):
+        m(q, q)
+    with pytest.raises(tta.GruTimeoutError):
+        tta.check_gru_status()
+    snap = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    opt.zero_grad()
+    crit(*m(q, q)).backward()
+    opt.step()
+    torch.cuda.synchronize()
+    assert any(not torch.equal(v, snap[k]) for k, v in m.state_dict().items())
 
 
 @pytest.mark.parametrize("H,depth", [(64, 4), (128, 4), (128, 1), (192, 4), (256, 2), (320, 4), (384, 4), (448, 4),

@@ -120,6 +120,27 @@ TT_DEV void st8_sc1(__amdgpu_buffer_rsrc_t r, int off, const float (&f)[8], bf16
   st16_sc1(r, off, make_uint4(w[0], w[1], w[2], w[3]));
 }
 
+// Full-line epilogue stores from a transposed-accumulate 16x16 tile pair. After the
+// column-pair v_permlane16_swap, lane l holds two 16-byte chunks of its row (l & 15): v0 =
+// 8 columns c.. of the pair's first 32 columns, v1 = the same 8 columns + 32; one store
+// instruction of them writes 16 rows x 64 B (16 half lines). row_pair exchanges v1 of rows
+// 0-7 with v0 of rows 8-15 (lane l <-> l ^ 8, one v_mov_dpp row_ror:8 per dword), so that
+// store `da` writes rows 0-7 whole (8 lanes x 16 B = 128 B per row) and `db` rows 8-15:
+// lane l stores da at row (l & 7), db at row (l & 7) + 8, both at column c + (l & 8 ? 32 : 0).
+TT_DEV uint32_t dpp_ror8(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128 /* row_ror:8 */, 0xF, 0xF, false);
+}
+TT_DEV void row_pair(const uint4& v0, const uint4& v1, uint4& da, uint4& db) {
+  const bool lo = (threadIdx.x & 8) == 0;
+  uint4 s = lo ? v1 : v0, r;
+  r.x = dpp_ror8(s.x);
+  r.y = dpp_ror8(s.y);
+  r.z = dpp_ror8(s.z);
+  r.w = dpp_ror8(s.w);
+  da = lo ? v0 : r;
+  db = lo ? r : v1;
+}
+
 // 8 elements held raw (16 B bf16 / 32 B fp32) so loads can be issued long before use.
 template <typename T>
 struct Raw8 {

@@ -112,6 +112,9 @@ constexpr int BM = 128, BN = 128;  // tile of the register-staged / small path
 // n-tile) with the n-tile fastest, so the tiles of one A panel, and all tiles of one
 // split-K slice, share an XCD's L2.
 using ttg::xcd_remap;
+#ifndef TT_EPI_PAIR  // 1: bf16 register-direct epilogues store whole 128-B lines (row_pair, tt_common.h)
+#define TT_EPI_PAIR 1
+#endif
 #ifndef TT_GEMM_BAL
 #define TT_GEMM_BAL true
 #endif
@@ -342,6 +345,34 @@ TT_DEV void epi_direct(const GemmArgs& g, const f32x4 (&acc)[8][4], TO* C, const
   for (int i = 0; i < 8; ++i) {
     const int gm = m0 + wm + 16 * i + lr;
     if constexpr (sizeof(TO) == 2) {
+#if TT_EPI_PAIR
+      if (full) {  // whole 128-B lines: 8 rows per store instruction (row_pair)
+        uint4 v[2];
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          uint32_t w[2][2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int j = 2 * jp + h, c = n0 + wn + 16 * j + 4 * q;
+            float x[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[e] = fin(acc[i][j][e], bv[j][e], gm, c + e);
+            w[h][0] = (uint32_t)f2bf(x[0]) | ((uint32_t)f2bf(x[1]) << 16);
+            w[h][1] = (uint32_t)f2bf(x[2]) | ((uint32_t)f2bf(x[3]) << 16);
+          }
+          const auto s0 = __builtin_amdgcn_permlane16_swap(w[0][0], w[1][0], false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(w[0][1], w[1][1], false, false);
+          v[jp] = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        }
+        uint4 da, db;
+        row_pair(v[0], v[1], da, db);
+        const int ra = m0 + wm + 16 * i + (lr & 7);
+        const int cs = n0 + wn + 16 * (q & 1) + 8 * (q >> 1) + (lr & 8 ? 32 : 0);
+        put(ra, cs, da);
+        put(ra + 8, cs, db);
+        continue;
+      }
+#endif
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp) {
         uint32_t w[2][2];
@@ -413,6 +444,9 @@ TT_DEV void epi_direct(const GemmArgs& g, const f32x4 (&acc)[8][4], TO* C, const
 #endif
 #ifndef BRES_PD  // gemm_bres A prefetch: 1 a whole tile ahead, 0 half a tile
 #define BRES_PD 1
+#endif
+#ifndef BRES_PAIR  // 1: gemm_bres stores whole 128-B lines (row_pair) -- slower, off
+#define BRES_PAIR 0
 #endif
 #ifndef BRES_STAG  // waves 4-7 start BRES_STAG x 64 cycles late (0: together)
 #define BRES_STAG 0
@@ -504,6 +538,38 @@ __global__ __launch_bounds__(512, 1) void gemm_bres(GemmArgs g, int npan, int nb
     for (int rb = 0; rb < 2; ++rb) {
       const int row = t * 32 + rb * 16 + lr;
       const bool ok = g0 + row < g.M;
+#if BRES_PAIR && !(BRES_DIAG & 1) && BRES_STORE == 0  // measured slower: 3.33 vs 2.89 ms (profiles/r06_epi_pair_ab.txt)
+      if (g0 + t * 32 + rb * 16 + 16 <= g.M) {  // whole 128-B lines: 8 rows per store (row_pair)
+#pragma unroll
+        for (int a = 0; a < BR_COLS / 64; ++a) {
+          uint4 v[2];
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int jp = 2 * a + u;
+            uint32_t w[2][2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int j = 2 * jp + h;
+              const float4 b4 = *reinterpret_cast<const float4*>(bias_s + 16 * j + 4 * q);
+              const float v0 = acc[rb][j][0] + b4.x, v1 = acc[rb][j][1] + b4.y;
+              const float v2 = acc[rb][j][2] + b4.z, v3 = acc[rb][j][3] + b4.w;
+              w[h][0] = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+              w[h][1] = (uint32_t)f2bf(v2) | ((uint32_t)f2bf(v3) << 16);
+            }
+            const auto s0 = __builtin_amdgcn_permlane16_swap(w[0][0], w[1][0], false, false);
+            const auto s1 = __builtin_amdgcn_permlane16_swap(w[0][1], w[1][1], false, false);
+            v[u] = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+          }
+          uint4 da, db;
+          row_pair(v[0], v[1], da, db);
+          const long ra = g0 + t * 32 + rb * 16 + (lr & 7);
+          const int cs = n0 + 64 * a + 16 * (q & 1) + 8 * (q >> 1) + (lr & 8 ? 32 : 0);
+          *reinterpret_cast<uint4*>(C + ra * g.ldc + cs) = da;
+          *reinterpret_cast<uint4*>(C + (ra + 8) * g.ldc + cs) = db;
+        }
+        continue;
+      }
+#endif
 #pragma unroll
       for (int jp = 0; jp < BR_COLS / 32; ++jp) {
         uint32_t w[2][2];

@@ -21,6 +21,19 @@ class Adam(torch.optim.Optimizer):
         if lr < 0.0 or eps < 0.0 or not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0:
             raise ValueError("invalid Adam hyper-parameter")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self._guard_reads = []  # (event, pinned int32[1] copy of the guard, params) per earlier launch
+
+    def settle_skipped_steps(self):
+        """Take every earlier step that the device skipped (its step guard was set) off the
+        step counters of the parameters it covered, so Adam's bias correction counts applied
+        updates only. Called by step(); waits for the earlier steps' launches (the host is
+        normally a whole forward and backward ahead of them, so this rarely blocks)."""
+        reads, self._guard_reads = self._guard_reads, []
+        for ev, word, plist in reads:
+            ev.synchronize()
+            if int(word.item()) != 0:
+                for p in plist:
+                    self.state[p]["step"] -= 1
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -28,6 +41,8 @@ class Adam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        self.settle_skipped_steps()
+        stepped = {}  # device -> parameters launched this step
         for group in self.param_groups:
             ps = [p for p in group["params"] if p.grad is not None]
             if not ps:
@@ -63,7 +78,14 @@ class Adam(torch.optim.Optimizer):
             # the kernel writes through raw pointers: record the in-place update for autograd
             # and for the packed-weight cache of the towers (towers._packed)
             torch.autograd.graph.increment_version(ps)
-        for g in {towers.step_guard(p.device) for group in self.param_groups for p in group["params"]
-                  if p.grad is not None}:
-            g.zero_()  # stream-ordered after every launch above
+            stepped.setdefault(dev, []).extend(ps)
+        for dev, plist in stepped.items():
+            g = towers.step_guard(dev)
+            with torch.cuda.device(dev):
+                word = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+                word.copy_(g, non_blocking=True)  # did the device skip this step? (settle_skipped_steps)
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(dev))
+                g.zero_()  # stream-ordered after every launch above
+            self._guard_reads.append((ev, word, plist))
         return loss

@@ -176,9 +176,16 @@ def _alloc(shape, dt, dev):
 #    forward (waiting on its event: the host is at most the GPU's queue ahead, which still
 #    holds later work, so the GPU never idles for it), TowersFn.backward the ones already
 #    finished.
+# The guard is armed only by forwards that record autograd state (an eval / no-grad forward
+# feeds no optimiser step), and once check_gru_status has reported a timeout to the host the
+# guard of that device is cleared, stream-ordered, by the next forward: from then on the host
+# owns the recovery, and a healthy step after it trains. two_towers_amd.Adam does not count a
+# step the device skipped (it reads each step's guard back asynchronously and takes the step
+# off the parameters' step counters at its next call).
 _status_lock = threading.Lock()
-_status_pending: list = []  # (event, pinned int32[1])
+_status_pending: list = []  # (event, pinned int32[1], device)
 _step_guard: dict = {}  # device -> int32[1]: OR of the status words since the last optimiser step
+_guard_reset: set = set()  # devices whose timeout the host has been told of: cleared at the next forward
 
 
 def step_guard(dev) -> torch.Tensor:
@@ -205,19 +212,33 @@ def gru_fwd_workspace(nrec, B, T, H, dt, dev):
     return ws
 
 
-def watch_gru_status(ws):
+def reset_guard_if_reported(dev):
+    """Before a forward's launches: clear the device's step guard (stream-ordered) if the host
+    has been told of a timed-out forward since the guard was last cleared."""
+    dev = torch.device(dev)
+    with _status_lock:
+        due = dev in _guard_reset
+        _guard_reset.discard(dev)
+    if due:
+        with torch.cuda.device(dev):
+            step_guard(dev).zero_()
+
+
+def watch_gru_status(ws, arm: bool = True):
     """After the launches using ws (on its device's current stream): fold its status word
-    into the device's step guard and queue an asynchronous read-back for the host."""
+    into the device's step guard (arm: the forward records autograd state, so an optimiser
+    step may follow) and queue an asynchronous read-back for the host."""
     with torch.cuda.device(ws.device):
         st = torch.cuda.current_stream(ws.device)
         word = ws[:4].view(torch.int32)
-        step_guard(ws.device).bitwise_or_(word)
+        if arm:
+            step_guard(ws.device).bitwise_or_(word)
         host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         host.copy_(word, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(st)
     with _status_lock:
-        _status_pending.append((ev, host))
+        _status_pending.append((ev, host, torch.device(ws.device)))
 
 
 def check_gru_status(wait: bool = True):
@@ -228,15 +249,19 @@ def check_gru_status(wait: bool = True):
         _status_pending.clear()
     bad = 0
     keep = []
-    for ev, host in pend:
+    bad_devs = set()
+    for ev, host, dev in pend:
         if not wait and not ev.query():
-            keep.append((ev, host))
+            keep.append((ev, host, dev))
             continue
         ev.synchronize()
-        bad += int(host.item() != 0)
-    if keep:
-        with _status_lock:
+        if host.item() != 0:
+            bad += 1
+            bad_devs.add(dev)
+    with _status_lock:
+        if keep:
             _status_pending[:0] = keep
+        _guard_reset.update(bad_devs)
     if bad:
         raise _lib.GruTimeoutError(
             f"{bad} column-split GRU forward launch(es) timed out waiting for a member workgroup "
@@ -437,6 +462,7 @@ class TowersFn(torch.autograd.Function):
         check_gru_status(wait=True)  # every earlier forward's column-split launches
         dt, E, H, h = cfg.dtype, cfg.E, cfg.H, cfg.h
         dev = xs[0].device
+        reset_guard_if_reported(dev)
         B, T = xs[0].shape[0], xs[0].shape[1]
         for x in xs:
             if x.shape[0] != B or x.shape[1] != T:
@@ -453,7 +479,8 @@ class TowersFn(torch.autograd.Function):
         Xl1 = X1 if train_drop else Y0
         Y1, _, S1 = _gru_layer_fwd(cfg, Xl1, 2 * H, 2 * H, packs, 1, B, T, seeds, False, ws)
         if ws is not None:
-            watch_gru_status(ws)
+            # only a forward that records autograd state arms the optimiser's step guard
+            watch_gru_status(ws, arm=any(ctx.needs_input_grad))
         # cat(h_fwd at t=T-1, h_rev at t=0) -> [B, 2H] (enhanced_two_tower.py:53,59)
         hcat = []
         for ti in range(n):

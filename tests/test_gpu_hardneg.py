@@ -121,6 +121,46 @@ def test_hardneg_scan_matches_gemm_path(B, nd, h, lab):
     assert torch.equal(si, gi)
 
 
+def _scan_with_cm(q, d, lab, k):
+    """tt_hardneg_topk with the workspace kept: (idx, val, chunk maxima [B, nch])."""
+    lib = _lib.load()
+    B, h = q.shape
+    nd = d.shape[0]
+    dt = torch.bfloat16
+    qd, dd = q.to(DEV, dt).contiguous(), d.to(DEV, dt).contiguous()
+    idx = torch.empty(B, k, dtype=torch.int32, device=DEV)
+    val = torch.empty(B, k, dtype=torch.float32, device=DEV)
+    ws = torch.full((lib.tt_hardneg_ws_size(dtype_code(dt), B, nd, h, k),), 0x7F, dtype=torch.uint8, device=DEV)
+    call("tt_hardneg_topk", dtype_code(dt), qd.data_ptr(), B, dd.data_ptr(), nd, h, lab, k, idx.data_ptr(),
+         val.data_ptr(), ws.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    nch = (nd + 63) // 64
+    return idx.cpu(), val.cpu(), ws[:B * nch * 4].view(torch.float32).view(B, nch).cpu()
+
+
+@pytest.mark.parametrize("B,nd,h,lab,k", [(8192, 8192, 256, 0, 5), (1000, 3000, 256, 0, 5), (513, 513, 256, 0, 5),
+                                          (300, 4100, 128, -1, 16), (64, 4096, 256, 1024, 5), (129, 4100, 512, 7, 16),
+                                          (2048, 16384, 256, 100, 5), (40, 70, 128, 3, 1)])
+def test_hardneg_scan_gemm_matches_scan_kernel(B, nd, h, lab, k):
+    """The scan's chunk maxima from the persistent 256x256 GEMM with the chunk-max epilogue
+    (option hn_scan_gemm 1, the default: tt_gemm.hip gemm_persist HN) against the streamed
+    scan kernel (hn_scan_gemm 0): the same MFMA instruction, operand orientation and k order,
+    so every chunk maximum -- masked positive (-1) and tail columns (-inf) included -- and
+    therefore every index and value is bit-identical. Ragged row tiles, partial chunks, label
+    offsets, nothing masked, h 128 / 256 / 512, k 1 / 5 / 16."""
+    g = torch.Generator().manual_seed(B + nd + h + k)
+    q = torch.nn.functional.normalize(torch.randn(B, h, generator=g), dim=1)
+    d = torch.nn.functional.normalize(torch.randn(nd, h, generator=g), dim=1)
+    with option("hn_scan_gemm", 0):
+        ki, kv, kcm = _scan_with_cm(q, d, lab, k)
+    with option("hn_scan_gemm", 1):
+        gi, gv, gcm = _scan_with_cm(q, d, lab, k)
+    assert torch.equal(kcm.view(torch.int32), gcm.view(torch.int32)), int((kcm != gcm).sum())
+    assert torch.equal(ki, gi) and torch.equal(kv, gv)
+    ri, rv = ref_hardneg(q.to(torch.bfloat16).float(), d.to(torch.bfloat16).float(), lab, k)
+    assert float((gv.double() - rv).abs().max()) < 1e-5  # fp32 accumulation of bf16 products
+
+
 @pytest.mark.parametrize("B,nd,lab", [(8192, 8192, 0), (2048, 16384, 100), (1000, 3000, 0)])
 @pytest.mark.parametrize("hn_map", [1, 2])
 def test_hardneg_scan_block_maps_agree(B, nd, lab, hn_map):
@@ -130,9 +170,10 @@ def test_hardneg_scan_block_maps_agree(B, nd, lab, hn_map):
     g = torch.Generator().manual_seed(B + nd + hn_map)
     q = torch.nn.functional.normalize(torch.randn(B, 256, generator=g), dim=1)
     d = torch.nn.functional.normalize(torch.randn(nd, 256, generator=g), dim=1)
-    si, sv = run_hardneg(q, d, lab, 5, torch.bfloat16)
-    with option("hn_map", hn_map):
-        mi, mv = run_hardneg(q, d, lab, 5, torch.bfloat16)
+    with option("hn_scan_gemm", 0):  # the block maps are the scan kernel's
+        si, sv = run_hardneg(q, d, lab, 5, torch.bfloat16)
+        with option("hn_map", hn_map):
+            mi, mv = run_hardneg(q, d, lab, 5, torch.bfloat16)
     assert torch.equal(sv, mv)
     assert torch.equal(si, mi)
 

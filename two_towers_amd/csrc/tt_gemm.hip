@@ -1,5 +1,6 @@
 // Generic batched MFMA GEMM (NT / NN / TN, optional split-K) and the C-ABI
 // entry points tt_gemm / tt_gemm_ws_size / tt_gemm_pick_splits.
+#include <float.h>
 #include <stdarg.h>
 #include <stdlib.h>
 
@@ -40,7 +41,7 @@ constexpr OptDef kOpts[OPT_N] = {
     {"gru_fwd_skew", "TT_GRU_FWD_SKEW", 0},       {"gemm_bres", "TT_GEMM_BRES", 1},
     {"gru_xc_coop", "TT_GRU_XC_COOP", 0},         {"gemm_buf", "TT_GEMM_BUF", 1},
     {"gemm_order", "TT_GEMM_ORDER", 0},           {"gru_step_ring", "TT_GRU_STEP_RING", 4},
-    {"gru_fwd_xs", "TT_GRU_FWD_XS", 1},
+    {"gru_fwd_xs", "TT_GRU_FWD_XS", 1},           {"hn_scan_gemm", "TT_HN_SCAN_GEMM", 1},
 };
 struct OptTable {
   std::atomic<int> v[OPT_N];
@@ -104,6 +105,11 @@ struct GemmArgs {
   int stream_out;   // write-through (sc1) output stores: big outputs
   int walk_g, walk_x;  // gemm_persist tile walk: column panels per group, workgroup sets (0: default)
   int nbatch;
+  // gemm_persist<..., HN>: the hard-negative scan's epilogue (tt_score.hip): per (row, 64-column
+  // chunk) only the maximum leaves, into cm[row * nch + chunk]; column label_off + row scores
+  // -1 (the positive), columns >= N -inf
+  float* cm;
+  long nch, label_off;
 };
 
 constexpr int BM = 128, BN = 128;  // tile of the register-staged / small path
@@ -112,6 +118,9 @@ constexpr int BM = 128, BN = 128;  // tile of the register-staged / small path
 // n-tile) with the n-tile fastest, so the tiles of one A panel, and all tiles of one
 // split-K slice, share an XCD's L2.
 using ttg::xcd_remap;
+#ifndef PERSIST_BAL  // 1: gemm_persist (A3) reads its fragments in the balanced 12/4/8 order of Loop8::run3
+#define PERSIST_BAL 1
+#endif
 #ifndef TT_EPI_PAIR  // 1: bf16 register-direct epilogues store whole 128-B lines (row_pair, tt_common.h)
 #define TT_EPI_PAIR 1
 #endif
@@ -422,6 +431,61 @@ TT_DEV void epi_direct(const GemmArgs& g, const f32x4 (&acc)[8][4], TO* C, const
   }
 }
 
+// ---- chunk-max epilogue of the hard-negative scan (gemm_persist HN) --------------------
+// The wave's 128 x 64 block (CT: acc[i][j][r] = C(wm + 16i + (lane & 15), wn + 16j + 4q + r))
+// is exactly one 64-column chunk of 128 query rows: per row the 16 lane-local values, then
+// the maximum over the four lane groups q (v_permlane16/32_swap), so every lane holds its
+// row's chunk maximum; lane group q stores rows i = 2q, 2q + 1 (2 stores per wave). Masked
+// form (a tile holding a positive column or columns past N): the positive scores -1, columns
+// past N -inf -- get_hard_negatives's sims[positive_idx] = -1 (enhanced_two_tower.py:130).
+TT_DEV float rowgroup_max4(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+TT_DEV void epi_chunkmax(const GemmArgs& g, const f32x4 (&acc)[8][4], int m0, int n0, int wm, int wn) {
+  const int lane = threadIdx.x & 63, q = lane >> 4, lr = lane & 15;
+  const int c0 = n0 + wn;  // the wave's chunk starts here
+  const bool masked = (g.label_off >= 0 && g.label_off + m0 + wm < c0 + 64 && c0 < g.label_off + m0 + wm + 128) ||
+                      c0 + 64 > g.N;
+  float mx[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[4 * j + r] = acc[i][j][r];
+    if (masked) {
+      const long lab = g.label_off >= 0 ? g.label_off + m0 + wm + 16 * i + lr : -1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int col = c0 + 16 * j + 4 * q + r;
+          if (col == lab) v[4 * j + r] = -1.f;
+          if (col >= g.N) v[4 * j + r] = -FLT_MAX;
+        }
+    }
+    float m = fmaxf(fmaxf(v[0], v[1]), v[2]);
+#pragma unroll
+    for (int e = 3; e < 15; e += 2) m = fmaxf(fmaxf(m, v[e]), v[e + 1]);
+    mx[i] = rowgroup_max4(fmaxf(m, v[15]));
+  }
+  const long chunk = c0 / 64;
+  if (chunk >= g.nch) return;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = 2 * q + u;
+    float m = mx[0];
+#pragma unroll
+    for (int e = 1; e < 8; ++e) m = i == e ? mx[e] : m;
+    const long row = (long)m0 + wm + 16 * i + lr;
+    if (row < g.M) g.cm[row * g.nch + chunk] = m;
+  }
+}
+
 // ---- B-resident short-K GEMM (the GRU's layer-0 input projection) ----------------------
 // C_b[m][n] = A_b[m][:K] . B_b[n][:K] + bias_b[n], bf16 in and out, fp32 accumulation,
 // K <= 384 and a multiple of 32, N a multiple of 192 (input_proj_l0: M = B*T, N = 6H =
@@ -614,8 +678,9 @@ __global__ __launch_bounds__(512, 1) void gemm_bres(GemmArgs g, int npan, int nb
 // first counted wait of the next tile lets the epilogue's stores stay in flight. Measured
 // before this: the LDS-staged epilogue plus its barriers cost ~20k cycles per tile, more
 // than the 5 K-tiles of MFMAs of input_proj_l0.
-template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO, bool A3, bool BUF = false>
+template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO, bool A3, bool BUF = false, bool HN = false>
 __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
+  static_assert(!HN || (A3 && !AKO && !BKO && !SHIFT), "the scan epilogue runs on the A3 direct-epilogue form");
   using L8 = ttg::Loop8<T, AKO, BKO, false, A3, A3, BUF>;  // A3: transposed accumulate, direct epilogue
   using Piece = typename L8::Piece;
   constexpr int STG = A3 ? 0 : 32 * 256 * 4;
@@ -763,6 +828,39 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
           pa1.init(la, 0, nk, g.K, 128);
           ra_off = nk;
         }
+#if PERSIST_BAL
+        // balanced fragment reads (the run3 schedule): P1 A rows 0-63 + B columns 0-31 (12
+        // reads), P2 B columns 32-63 (4), P3 A rows 64-127 (8); B is last read in P2, so both
+        // B halves of K-tile r+2 are restaged in P4, two phases later
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) fa[ks][i] = ttg::frag2<T, AKO>(ia, 16 * i, ks);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) fb[ks][j] = ttg::frag2<T, BKO>(ib, bc + 16 * j, ks);
+        }
+        pa0.issue(r + 2 - ra_off, anx);
+        L8::quad(0, 0, fa, fb, acc);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int j = 2; j < 4; ++j) fb[ks][j] = ttg::frag2<T, BKO>(ib, bc + 16 * j, ks);
+        pa1.issue(r + 2 - ra_off, anx + L8::HALF);
+        L8::quad(0, 1, fa, fb, acc);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) fa[ks][i] = ttg::frag2<T, AKO>(ia, 64 + 16 * i, ks);
+        L8::quad(1, 1, fa, fb, acc);
+        if (r + 2 == nk) {
+          lb = loader_b(qn);
+          pb0.init(lb, 0, nk, g.K, 0);
+          pb1.init(lb, 0, nk, g.K, 128);
+          rb_off = nk;
+        }
+        pb0.issue(r + 2 - rb_off, bcur);
+        pb1.issue(r + 2 - rb_off, bcur + L8::HALF);
+#else
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
@@ -787,6 +885,7 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
         pb0.issue(r + 2 - rb_off, bcur);
         L8::quad(1, 1, fa, fb, acc);
         pb1.issue(r + 2 - rb_off, bcur + L8::HALF);
+#endif
         // K-tile r+1 landed; the 8 DMAs of r+2 stay in flight, and at r = 0 also the
         // previous tile's epilogue stores (issued after r+1's DMAs, before r+2's)
 #ifdef TT_DIAG
@@ -794,7 +893,11 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
 #else
         constexpr bool loose = false;
 #endif
-        if ((r == 0 && epi_full) || loose) {
+        if constexpr (HN) {
+          // the scan's 2 chunk-max stores of the previous tile stay in flight at r = 0
+          if (r == 0 && epi_full) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else if ((r == 0 && epi_full) || loose) {
           if constexpr (EPI_STORES<TO> == 16) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
           else asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
         } else {
@@ -807,6 +910,12 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
       rb_off -= nk;
       // epilogue straight from the accumulators: no LDS, no barrier, so the K-tile stream
       // (and the two wave rows' one-barrier stagger) runs on into tile qn unchanged
+      if constexpr (HN) {
+        epi_chunkmax(g, acc, cur_t.m0, cur_t.n0, wm, wn);
+        // 2 stores per wave unless the wave's chunk or rows lie wholly past the ends
+        epi_full = __builtin_amdgcn_readfirstlane((int)(cur_t.m0 + 256 <= g.M && cur_t.n0 + 256 <= 64 * g.nch)) != 0;
+        continue;
+      }
       const bool full = cur_t.m0 + 256 <= g.M && cur_t.n0 + 256 <= g.N && g.vec_ok;
       epi_direct<TO>(g, acc, static_cast<TO*>(g.c[cur_t.bi]), g.bias[cur_t.bi], cur_t.m0, cur_t.n0, wm, wn, full);
       epi_full = __builtin_amdgcn_readfirstlane((int)full) != 0;
@@ -1080,6 +1189,41 @@ int launch_gemm(int akout, int bkout, bool shift, GemmArgs& g, int nbatch, hipSt
 }
 
 }  // namespace
+
+// Step 1 of the hard-negative top-k (tt_score.hip) on the persistent 256x256 GEMM:
+// S = Q D^T (bf16, K = h a multiple of 64) accumulated transposed -- the hn_scan kernel's MFMA
+// orientation, instruction and k order, so the chunk maxima are the values hn_rescore
+// recomputes bit for bit -- with the chunk-max epilogue instead of C stores. Tiles in column
+// groups per XCD (gemm_order's walk) when the shape allows.
+int tt::tt_hn_scan_gemm(const void* q, long bq, const void* d, long nd, int h, long label_off, float* cm, long nch,
+                    hipStream_t st) {
+  TT_CHECK_ARG(h % 64 == 0 && h <= 1024 && bq > 0 && nd > 0 && bq < (1L << 31) && nd < (1L << 31),
+               "tt_hn_scan_gemm: h %d, bq %ld, nd %ld", h, bq, nd);
+  GemmArgs g{};
+  g.a[0] = q;
+  g.b[0] = d;
+  g.lda = g.ldb = h;
+  g.M = (int)bq;
+  g.N = (int)nd;
+  g.K = h;
+  g.alpha = 1.f;
+  g.splits = 1;
+  g.kt_per_split = h / 64;
+  g.nbatch = 1;
+  g.cm = cm;
+  g.nch = nch;
+  g.label_off = label_off;
+  const long ntm = (bq + 255) / 256, ntn = (nd + 255) / 256, ntiles = ntm * ntn;
+  TT_CHECK_ARG(ntiles < (1L << 31), "tt_hn_scan_gemm: too many tiles");
+  if (ntiles % 256 == 0 && ntn % 4 == 0) {
+    g.walk_g = 4;
+    g.walk_x = 8;
+  }
+  hipLaunchKernelGGL((gemm_persist<bf16_t, false, false, false, float, true, true, true>),
+                     dim3((unsigned)std::min<long>(ntiles, 256)), dim3(512), 0, st, g, (int)ntiles);
+  TT_CHECK_LAUNCH("gemm_persist (hard-negative scan)");
+  return 0;
+}
 
 extern "C" long tt_gemm_ws_size(int m, int n, int nbatch, int splits) {
   (void)m;

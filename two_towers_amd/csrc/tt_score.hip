@@ -550,11 +550,18 @@ int hn_run(const bf16_t* qn, long bq, const bf16_t* dn, long nd, long label_offs
   int32_t* sel = reinterpret_cast<int32_t*>(ws + p.off_sel);
   float* cand = reinterpret_cast<float*>(ws + p.off_cand);
   const int nsel = (int)(p.nch < k ? p.nch : k);
-  int map = tt::opt(tt::OPT_HN_MAP);
-  if (map == 2 && (p.RT % 2 != 0 || p.S % 4 != 0)) map = 0;
-  hipLaunchKernelGGL((hn_scan_kernel<KS>), dim3((unsigned)(p.RT * p.S)), dim3(ScanCfg<KS>::WAVES * 64), 0, st, qn, bq, dn, nd, label_offset, (int)p.S,
-                     (int)p.tps, p.nch, CM, map);
-  TT_CHECK_LAUNCH("hn_scan_kernel");
+  if (tt::opt(tt::OPT_HN_SCAN_GEMM) && (32 * KS) % 64 == 0) {
+    // the same chunk maxima from the persistent 256x256 GEMM (tt_gemm.hip gemm_persist HN):
+    // same MFMA, operand orientation and k order as hn_scan_kernel, so hn_rescore below
+    // still reproduces every ranked value bit for bit
+    TT_PROPAGATE(tt::tt_hn_scan_gemm(qn, bq, dn, nd, 32 * KS, label_offset, CM, p.nch, st));
+  } else {
+    int map = tt::opt(tt::OPT_HN_MAP);
+    if (map == 2 && (p.RT % 2 != 0 || p.S % 4 != 0)) map = 0;
+    hipLaunchKernelGGL((hn_scan_kernel<KS>), dim3((unsigned)(p.RT * p.S)), dim3(ScanCfg<KS>::WAVES * 64), 0, st, qn, bq, dn, nd, label_offset, (int)p.S,
+                       (int)p.tps, p.nch, CM, map);
+    TT_CHECK_LAUNCH("hn_scan_kernel");
+  }
   const dim3 rows4((unsigned)tt_ceil_div(bq, 4));
   if (k <= 8)
     hipLaunchKernelGGL((hn_select_kernel<8>), rows4, dim3(256), 0, st, CM, bq, p.nch, k, sel);

@@ -21,7 +21,8 @@ master weights whose forward sees their bf16 rounding (the compute precision of 
 under test). Stored: the per-step losses and mined indices, and for every parameter 64
 fixed positions of its initial and final values plus the norm of its total change, and per step
 the oracle's gap between each row's k-th and (k+1)-th best cosine (how far from a tie the
-mined set is).
+mined set is) and each row's 16 best negatives with their cosines (so a GPU pick that differs
+can be checked to be a near-tie of the oracle's ranking).
 """
 from __future__ import annotations
 
@@ -80,6 +81,15 @@ def make_batches(b=B, seed=SEED_DATA, n=2):
     return out
 
 
+def top16(rq, rd):
+    """Per row: the oracle's 16 best in-batch negatives (positive masked) and their cosines."""
+    with torch.no_grad():
+        cos = cpu_ref.normalize(rq.detach(), 1e-8) @ cpu_ref.normalize(rd.detach(), 1e-8).t()
+        cos.fill_diagonal_(-1.0)
+        t = cos.topk(16, dim=1)
+    return t.indices.numpy().astype(np.int16), t.values.numpy().astype(np.float32)
+
+
 def tie_gaps(rq, rd, k=K):
     """Per row: cosine of the k-th best in-batch negative minus the (k+1)-th (positive
     masked), from the oracle's fp32 outputs."""
@@ -101,7 +111,7 @@ def main():
     pos = positions(p)
     master = {k: v.clone().requires_grad_(True) for k, v in p.items()}
     opt = torch.optim.Adam(list(master.values()), lr=LR)
-    losses, picks, gaps = [], [], []
+    losses, picks, gaps, tops = [], [], [], []
     for s in range(STEPS):
         q, d = batches[s % 2]
         opt.zero_grad()
@@ -109,6 +119,7 @@ def main():
         rq, rd = cpu_ref.forward(q, d, pb, drop_p=0.1, seeds=seeds[s])
         loss, idx = cpu_ref.hardneg_margin(rq, rd, K, 0.2)
         gaps.append(tie_gaps(rq, rd))
+        tops.append(top16(rq, rd))
         loss.backward()
         opt.step()
         losses.append(float(loss.detach()))
@@ -117,7 +128,8 @@ def main():
         print(f"step {s}: loss {losses[-1]:.6f}; k/k+1 gap median {np.median(gp):.3e}, "
               f"rows with gap < 5e-3: {np.mean(gp < 5e-3):.3f}", flush=True)
     out = {"losses": np.array(losses), "picks": np.stack(picks), "seeds": np.array(seeds, dtype=np.int64),
-           "gaps": np.stack(gaps).astype(np.float32)}
+           "gaps": np.stack(gaps).astype(np.float32),
+           "top16_idx": np.stack([t[0] for t in tops]), "top16_cos": np.stack([t[1] for t in tops])}
     for k, v in p.items():
         out[f"pos/{k}"] = pos[k]
         out[f"w0/{k}"] = v.reshape(-1)[pos[k]].numpy()

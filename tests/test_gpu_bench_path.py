@@ -372,10 +372,15 @@ def test_bench_composition_bf16_adam_trajectory_matches_oracle():
     on its own fp32 outputs: a near-tie picked differently moves a row's mean negative
     cosine by at most ~2e-2 / k, i.e. the loss by ~1e-5.
     Tolerances: per-step loss within 1e-2 relative (5e-3 at step 0, as the single-step
-    composition test); >= 90 % of the rows pick the oracle's set at EVERY step (round 5's
-    fixture, lr 1e-3 on uncorrelated pairs, drove the loss onto the 0.2 margin floor where
-    every document is a near-tie: 0.96 at step 0, 0.01 by step 9); the oracle's loss ends
-    below the 0.2 margin (the towers separate positives from negatives, no collapse); for every
+    composition test); at EVERY step, every pick outside the oracle's set is a near-tie of
+    the oracle's ranking at that step (its oracle cosine within 2e-2 of the oracle's k-th best;
+    the fixture holds each row's 16 best per step) and >= 90 % of the rows pick the oracle's
+    exact set at steps 0-1, >= 70 % after (the two trajectories' weights drift apart by a
+    fraction of their movement while a row's 5th and 6th best cosines are ~1e-3 apart at B 512:
+    measured 0.95, 0.92, then 0.71-0.81; round 5's fixture, lr 1e-3 on uncorrelated pairs,
+    drove the loss onto the 0.2 margin floor where every document is a near-tie: 0.96 at step
+    0, 0.01 by step 9); the oracle's loss ends below the 0.2 margin (the towers separate
+    positives from negatives, no collapse); for every
     tensor, at 64 fixed positions, the distance of the final weights from the oracle's at
     most 0.25 of the distance the oracle's ten steps moved them (Adam's early steps are
     ~lr * sign(g): an element whose gradient is near zero can move the other way)."""
@@ -392,7 +397,7 @@ def test_bench_composition_bf16_adam_trajectory_matches_oracle():
     crit = tta.HardNegativeMarginLoss(k=k, margin=0.2, compute_dtype=torch.bfloat16)
     opt = tta.Adam(m.parameters(), lr=lr)
     torch.manual_seed(gen_traj.SEED_DROP)  # the model draws each step's dropout seeds from this stream, as the oracle did
-    gl, agree = [], []
+    gl, agree, tiegap = [], [], []
     for s in range(steps):
         q, d = batches[s % 2]
         opt.zero_grad()
@@ -402,18 +407,28 @@ def test_bench_composition_bf16_adam_trajectory_matches_oracle():
         gl.append(float(loss.detach()))
         idx = crit.last_indices.long().cpu().numpy()
         ridx = gold["picks"][s].astype(np.int64)
-        agree.append(float(np.mean([set(idx[i]) == set(ridx[i]) for i in range(Bq)])))
+        same = np.array([set(idx[i]) == set(ridx[i]) for i in range(Bq)])
+        agree.append(float(same.mean()))
+        # every pick outside the oracle's set is a near-tie of the oracle's ranking at this step
+        kth = gold["top16_cos"][s][:, k - 1]
+        worst = 0.0
+        for i in np.nonzero(~same)[0]:
+            top = dict(zip(gold["top16_idx"][s][i].astype(np.int64).tolist(), gold["top16_cos"][s][i].tolist()))
+            for j in set(idx[i].tolist()) - set(ridx[i].tolist()):
+                worst = max(worst, float(kth[i] - top[j]) if j in top else float("inf"))
+        tiegap.append(worst)
     tta.check_gru_status()
     rl = gold["losses"]
     for s in range(steps):
         print(f"step {s}: loss {gl[s]:.6f} vs oracle {rl[s]:.6f} (rel {abs(gl[s] - rl[s]) / abs(rl[s]):.2e}), "
-              f"picks agree {agree[s]:.4f}")
+              f"picks agree {agree[s]:.4f}, worst near-tie gap {tiegap[s]:.2e}")
     assert float(rl.min()) > 0.01, "hinges inactive: the test would compare zeros"
     # the oracle's towers learn to rank each positive above its mined negatives (loss under the
     # 0.2 margin) instead of collapsing onto the margin floor, where every pick is a near-tie
     assert float(rl[-1]) < 0.2, float(rl[-1])
     for s in range(steps):
-        assert agree[s] >= 0.90, (s, agree[s])  # only near-ties may be picked differently
+        assert tiegap[s] <= 2e-2, (s, tiegap[s])  # a differing pick is always a near-tie ...
+        assert agree[s] >= (0.90 if s < 2 else 0.70), (s, agree[s])  # ... and most rows pick the same set
         tol = 5e-3 if s == 0 else 1e-2
         assert abs(gl[s] - rl[s]) <= tol * abs(rl[s]), (s, gl[s], rl[s])
     worst, wk = 0.0, ""

@@ -270,6 +270,33 @@ def test_column_split_member_timeout_is_reported_and_not_sticky():
     assert any(not torch.equal(v, snap[k]) for k, v in m.state_dict().items())
 
 
+def test_column_split_forward_beside_a_busy_stream_is_valid_or_reported():
+    """The column-split forward is a plain launch by default (option gru_xc_coop 0): the
+    occupancy query proves only that the grid fits an idle device, so kernels on another
+    stream can keep members from being co-resident. Then either the members still meet (the
+    other work drains first) and every output is bit-identical to the quiet-device run, or a
+    bounded wait gives up and the launch reports it in its status word -- never wrong outputs
+    silently (the status reaches the host as GruTimeoutError and the optimiser's step guard).
+    Here torch GEMMs fill every CU from a second stream while the forward is launched."""
+    B, T, H, ntow = 8192, 8, 512, 2
+    G, whh, bhn = _inputs(ntow, B, T, H, seed=21)
+    ref = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=1)  # per-step kernel: the bit-identical reference
+    a = torch.randn(8192, 8192, device=DEV).to(torch.bfloat16)
+    hog, fwd = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(hog):
+        for _ in range(12):
+            c = a @ a  # ~1 ms each on every CU
+    with torch.cuda.stream(fwd):
+        out = _run(ntow, B, T, H, G, whh, bhn, 0.1, step=0)
+    torch.cuda.synchronize()
+    del c
+    st = _status(out[4])
+    print(f"forward beside a busy stream: status {st}")
+    if st == 0:
+        _assert_equivalent(out, ref, B, T, H, bhn)
+
+
 @pytest.mark.parametrize("H,depth", [(64, 4), (128, 4), (128, 1), (192, 4), (256, 2), (320, 4), (384, 4), (448, 4),
                                      (512, 1)])
 def test_runtime_width_persistent_forward_matches_per_step(H, depth):

@@ -143,8 +143,8 @@ def _scan_with_cm(q, d, lab, k):
                                           (2048, 16384, 256, 100, 5), (40, 70, 128, 3, 1)])
 def test_hardneg_scan_gemm_matches_scan_kernel(B, nd, h, lab, k):
     """The scan's chunk maxima from the persistent 256x256 GEMM with the chunk-max epilogue
-    (option hn_scan_gemm 1, the default: tt_gemm.hip gemm_persist HN) against the streamed
-    scan kernel (hn_scan_gemm 0): the same MFMA instruction, operand orientation and k order,
+    (option hn_scan_gemm 1: tt_gemm.hip gemm_persist HN; measured slower, not the default)
+    against the streamed scan kernel (hn_scan_gemm 0, the default): the same MFMA instruction, operand orientation and k order,
     so every chunk maximum -- masked positive (-1) and tail columns (-inf) included -- and
     therefore every index and value is bit-identical. Ragged row tiles, partial chunks, label
     offsets, nothing masked, h 128 / 256 / 512, k 1 / 5 / 16."""

@@ -41,7 +41,7 @@ constexpr OptDef kOpts[OPT_N] = {
     {"gru_fwd_skew", "TT_GRU_FWD_SKEW", 0},       {"gemm_bres", "TT_GEMM_BRES", 1},
     {"gru_xc_coop", "TT_GRU_XC_COOP", 0},         {"gemm_buf", "TT_GEMM_BUF", 1},
     {"gemm_order", "TT_GEMM_ORDER", 0},           {"gru_step_ring", "TT_GRU_STEP_RING", 4},
-    {"gru_fwd_xs", "TT_GRU_FWD_XS", 1},           {"hn_scan_gemm", "TT_HN_SCAN_GEMM", 1},
+    {"gru_fwd_xs", "TT_GRU_FWD_XS", 1},           {"hn_scan_gemm", "TT_HN_SCAN_GEMM", 0},
 };
 struct OptTable {
   std::atomic<int> v[OPT_N];

@@ -157,7 +157,11 @@ int tt_gru_fwd_launches(int dtype, int T, int H);
 /* Device scratch (bytes, 0 = none used) that lets tt_gru_fwd run the column-split persistent
  * kernel for this call shape on the current device: bf16, H 256 / 512, a batch large enough
  * (or option gru_fwd_xc = 2), and every member workgroup co-resident (one per CU, checked
- * against the occupancy query and launched cooperatively). H/64 workgroups share a block of
+ * against the occupancy query; a plain launch by default, hipLaunchCooperativeKernel with
+ * option gru_xc_coop = 1). The occupancy check covers an idle device only: kernels of other
+ * streams may keep members from being co-resident, and then the bounded member waits give up
+ * and set the STATUS word below (outputs invalid, reported -- never silently wrong); callers
+ * that overlap other work with this launch should expect that. H/64 workgroups share a block of
  * batch rows, each keeps 64 units' W_hh rows in registers, and they exchange h every step
  * through ws: per-group arrival counters (zeroed by every call, stream-ordered) and exchange
  * images. ws: 256-byte aligned, one buffer per launch in flight (distinct streams need

@@ -266,8 +266,9 @@ def test_gemm_input_projection_l1_class_hand_written():
     hand-written persistent kernel (no vendor GEMM is linked, include/tt_hip.h): against
     fp32 math on the bf16 operands, and run to run bit-identical (the training step is
     deterministic)."""
+    from two_towers_amd._lib import option
     dt = torch.bfloat16
-    m, n, k = 70000, 3072, 1024
+    m, n, k = 70144, 3072, 1024  # whole 256-row tiles: the interleaved-epilogue form (option gemm_iepi) applies
     g = torch.Generator(device=DEV).manual_seed(61)
     A = [torch.randn(m, k, generator=g, device=DEV).to(dt) for _ in range(2)]
     B = [(torch.randn(n, k, generator=g, device=DEV) * k ** -0.5).to(dt) for _ in range(2)]
@@ -279,8 +280,16 @@ def test_gemm_input_projection_l1_class_hand_written():
                  out_dtype=dt, bias=bias, splits=1)
         torch.cuda.synchronize()
         outs.append(C)
+    # each tile's epilogue inside the next tile's first K-tile (gemm_iepi 1, the default) or
+    # after its own last K-tile (0): the same values, bit for bit
+    C0 = [torch.full((m, n), float("nan"), device=DEV, dtype=dt) for _ in range(2)]
+    with option("gemm_iepi", 0):
+        ops.gemm(A, B, C0, m=m, n=n, k=k, lda=k, ldb=k, ldc=n, a_kouter=False, b_kouter=False, dtype=dt,
+                 out_dtype=dt, bias=bias, splits=1)
+    torch.cuda.synchronize()
     rows = torch.randint(0, m, (1024,), generator=g, device=DEV)
     for i in range(2):
+        assert torch.equal(outs[0][i], C0[i]), "interleaved and trailing epilogues differ"
         assert torch.equal(outs[0][i], outs[1][i]), "input projection not run-to-run identical"
         assert not torch.isnan(outs[0][i]).any()
         ref = A[i][rows].float() @ B[i].float().t() + bias[i]

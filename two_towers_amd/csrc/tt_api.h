@@ -44,6 +44,7 @@ enum Opt {
   OPT_GRU_FWD_XS,       // 1: column-split forward with matrix and vector waves (gru_fwd_xs, H 512); 0: gru_fwd_xcp
   OPT_HN_SCAN_GEMM,     // 1: hard-negative scan on the persistent 256x256 GEMM with a chunk-max epilogue
                         // (bit-identical; measured slower: 44.8 vs 38.7 us at 8192^2 x 256); 0: hn_scan_kernel
+  OPT_GEMM_IEPI,        // 1: the persistent GEMM's plain bf16 bias epilogue interleaved into the next tile's first K-tile
   OPT_N
 };
 int opt(Opt o);

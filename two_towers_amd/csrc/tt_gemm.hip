@@ -42,6 +42,7 @@ constexpr OptDef kOpts[OPT_N] = {
     {"gru_xc_coop", "TT_GRU_XC_COOP", 0},         {"gemm_buf", "TT_GEMM_BUF", 1},
     {"gemm_order", "TT_GEMM_ORDER", 0},           {"gru_step_ring", "TT_GRU_STEP_RING", 4},
     {"gru_fwd_xs", "TT_GRU_FWD_XS", 1},           {"hn_scan_gemm", "TT_HN_SCAN_GEMM", 0},
+    {"gemm_iepi", "TT_GEMM_IEPI", 1},
 };
 struct OptTable {
   std::atomic<int> v[OPT_N];
@@ -118,6 +119,9 @@ constexpr int BM = 128, BN = 128;  // tile of the register-staged / small path
 // n-tile) with the n-tile fastest, so the tiles of one A panel, and all tiles of one
 // split-K slice, share an XCD's L2.
 using ttg::xcd_remap;
+#ifndef PERSIST_IEPI  // 1: gemm_persist (A3) runs each tile's epilogue inside the next tile's first K-tile
+#define PERSIST_IEPI 1
+#endif
 #ifndef PERSIST_BAL  // 1: gemm_persist (A3) reads its fragments in the balanced 12/4/8 order of Loop8::run3
 #define PERSIST_BAL 1
 #endif
@@ -297,9 +301,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_kernel(GemmArgs g) {
 template <typename TO>
 constexpr int EPI_STORES = sizeof(TO) == 2 ? 16 : 32;
 
-template <typename TO>
+// MI/NI (>= 0): only the accumulator quadrant rows 4 MI..4 MI+3, column pair NI (the Loop8
+// quad), for the persistent kernel's interleaved epilogue (PERSIST_IEPI); -1: the whole block.
+template <typename TO, int MI = -1, int NI = -1>
 TT_DEV void epi_direct(const GemmArgs& g, const f32x4 (&acc)[8][4], TO* C, const float* bias, int m0, int n0,
                        int wm, int wn, bool full) {
+  constexpr int I0 = MI < 0 ? 0 : 4 * MI, I1 = MI < 0 ? 8 : 4 * MI + 4;
+  constexpr int JP0 = NI < 0 ? 0 : NI, JP1 = NI < 0 ? 2 : NI + 1;
   const int lane = threadIdx.x & 63, q = lane >> 4, lr = lane & 15;
   float bv[4][4];
 #pragma unroll
@@ -308,7 +316,7 @@ TT_DEV void epi_direct(const GemmArgs& g, const f32x4 (&acc)[8][4], TO* C, const
     for (int e = 0; e < 4; ++e) bv[j][e] = 0.f;
   if (bias) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 2 * JP0; j < 2 * JP1; ++j) {
       const int c = n0 + wn + 16 * j + 4 * q;
       if (full && g.bias_vec_ok) {
         const float4 b4 = *reinterpret_cast<const float4*>(bias + c);
@@ -351,11 +359,11 @@ TT_DEV void epi_direct(const GemmArgs& g, const f32x4 (&acc)[8][4], TO* C, const
     else *reinterpret_cast<uint4*>(C + (long)gm * g.ldc + gn) = v;
   };
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = I0; i < I1; ++i) {
     const int gm = m0 + wm + 16 * i + lr;
     if constexpr (sizeof(TO) == 2) {
 #if TT_EPI_PAIR
-      if (full) {  // whole 128-B lines: 8 rows per store instruction (row_pair)
+      if (NI < 0 && full) {  // whole 128-B lines: 8 rows per store instruction (row_pair)
         uint4 v[2];
 #pragma unroll
         for (int jp = 0; jp < 2; ++jp) {
@@ -383,7 +391,7 @@ TT_DEV void epi_direct(const GemmArgs& g, const f32x4 (&acc)[8][4], TO* C, const
       }
 #endif
 #pragma unroll
-      for (int jp = 0; jp < 2; ++jp) {
+      for (int jp = JP0; jp < JP1; ++jp) {
         uint32_t w[2][2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -412,7 +420,7 @@ TT_DEV void epi_direct(const GemmArgs& g, const f32x4 (&acc)[8][4], TO* C, const
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 2 * JP0; j < 2 * JP1; ++j) {
         const int c = n0 + wn + 16 * j + 4 * q;
         float v[4];
 #pragma unroll
@@ -428,6 +436,40 @@ TT_DEV void epi_direct(const GemmArgs& g, const f32x4 (&acc)[8][4], TO* C, const
         }
       }
     }
+  }
+}
+
+// Quadrant epilogue of gemm_persist IE (interleaved): a full tile, alpha 1, bias, no relu /
+// dropout, bf16 out; rows 4 MI..4 MI+3 of the wave block, column pair NI: bias, bf16 pairs,
+// one v_permlane16_swap per dword, one 16-byte store per row block (write-through when sc1).
+template <int MI, int NI>
+TT_DEV void epi_quad_simple(const GemmArgs& g, const f32x4 (&acc)[8][4], bf16_t* C, const float* bias, int m0, int n0,
+                            int wm, int wn) {
+  const int lane = threadIdx.x & 63, q = lane >> 4, lr = lane & 15;
+  float bv[2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float4 b4 = bias ? *reinterpret_cast<const float4*>(bias + n0 + wn + 16 * (2 * NI + h) + 4 * q)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    bv[h][0] = b4.x; bv[h][1] = b4.y; bv[h][2] = b4.z; bv[h][3] = b4.w;
+  }
+  const __amdgpu_buffer_rsrc_t crs = tt_rsrc(C + (long)m0 * g.ldc + n0);
+  const int cs = wn + 16 * (2 * NI + (q & 1)) + 8 * (q >> 1);
+#pragma unroll
+  for (int i = 4 * MI; i < 4 * MI + 4; ++i) {
+    uint32_t w[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x4 a = acc[i][2 * NI + h];
+      w[h][0] = (uint32_t)f2bf(a[0] + bv[h][0]) | ((uint32_t)f2bf(a[1] + bv[h][1]) << 16);
+      w[h][1] = (uint32_t)f2bf(a[2] + bv[h][2]) | ((uint32_t)f2bf(a[3] + bv[h][3]) << 16);
+    }
+    const auto s0 = __builtin_amdgcn_permlane16_swap(w[0][0], w[1][0], false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(w[0][1], w[1][1], false, false);
+    const uint4 v = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+    const int off = (int)(((long)(wm + 16 * i + lr) * g.ldc + cs) * 2L);
+    if (g.stream_out) st16_sc1(crs, off, v);
+    else st16_buf(crs, (uint32_t)off, 0, v);
   }
 }
 
@@ -678,7 +720,8 @@ __global__ __launch_bounds__(512, 1) void gemm_bres(GemmArgs g, int npan, int nb
 // first counted wait of the next tile lets the epilogue's stores stay in flight. Measured
 // before this: the LDS-staged epilogue plus its barriers cost ~20k cycles per tile, more
 // than the 5 K-tiles of MFMAs of input_proj_l0.
-template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO, bool A3, bool BUF = false, bool HN = false>
+template <typename T, bool AKO, bool BKO, bool SHIFT, typename TO, bool A3, bool BUF = false, bool HN = false,
+          bool IE = false>
 __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
   static_assert(!HN || (A3 && !AKO && !BKO && !SHIFT), "the scan epilogue runs on the A3 direct-epilogue form");
   using L8 = ttg::Loop8<T, AKO, BKO, false, A3, A3, BUF>;  // A3: transposed accumulate, direct epilogue
@@ -804,17 +847,45 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
   int as = 0;   // A3: A slot of the stream's current K-tile (git mod 3)
   int ra_off = 0, rb_off = 0;  // K-tile index of the A / B pieces' tile start in this tile's terms
   bool epi_full = false;       // A3: the previous tile's epilogue issued EPI_STORES<TO> stores per wave
+  // IEPI: the epilogue of tile i runs inside the first K-tile of tile i + 1, each accumulator
+  // quadrant just before the phase whose MFMAs first overwrite it (the quad order (0,0),
+  // (0,1), (1,1), (1,0)), so one wave row's epilogue arithmetic and stores overlap the other
+  // row's MFMAs instead of all 8 waves leaving the matrix pipe idle between tiles; the last
+  // quadrant's stores follow K-tile 2's DMAs and may stay in flight into K-tile 1's wait
+  constexpr bool IEPI = IE && A3 && !HN && PERSIST_BAL && std::is_same<TO, bf16_t>::value;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  TileId prev_t{0, 0, 0};
+  bool have_prev = false;
+  // the quadrant's epilogue of the previous tile, then its accumulators cleared
+  auto iepi = [&](auto mi_c, auto ni_c) {
+    constexpr int MI = decltype(mi_c)::value, NI = decltype(ni_c)::value;
+    if constexpr (IEPI)
+      epi_quad_simple<MI, NI>(g, acc, static_cast<bf16_t*>(g.c[prev_t.bi]), g.bias[prev_t.bi], prev_t.m0, prev_t.n0,
+                              wm, wn);
+#pragma unroll
+    for (int i = 4 * MI; i < 4 * MI + 4; ++i)
+#pragma unroll
+      for (int j = 2 * NI; j < 2 * NI + 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
   for (int q = qbeg; q < qend; q += qstep) {
     const int qn = q + qstep;
     const TileId cur_t = decode(q);
-    f32x4 acc[8][4];
+    if constexpr (!IEPI) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     uint4 fa[2][4], fb[2][4];
     if constexpr (A3) {
       for (int r = 0; r < nk; ++r, ++git) {
+        const bool ep = IEPI && r == 0 && have_prev;  // wave-uniform
         const int an = as == 0 ? 2 : as - 1;  // slot of K-tile r+2 = slot of r-1
         const int bs = git & 1;
         const char* ia = lds + as * (2 * L8::HALF) + wr * L8::HALF;
@@ -832,6 +903,10 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
         // balanced fragment reads (the run3 schedule): P1 A rows 0-63 + B columns 0-31 (12
         // reads), P2 B columns 32-63 (4), P3 A rows 64-127 (8); B is last read in P2, so both
         // B halves of K-tile r+2 are restaged in P4, two phases later
+        // (IEPI: each quadrant's epilogue before the phase's fragment reads, when the fewest
+        // fragment registers are live)
+        if constexpr (IEPI)
+          if (ep) iepi(C0{}, C0{});
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
@@ -841,12 +916,16 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
         }
         pa0.issue(r + 2 - ra_off, anx);
         L8::quad(0, 0, fa, fb, acc);
+        if constexpr (IEPI)
+          if (ep) iepi(C0{}, C1{});
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
           for (int j = 2; j < 4; ++j) fb[ks][j] = ttg::frag2<T, BKO>(ib, bc + 16 * j, ks);
         pa1.issue(r + 2 - ra_off, anx + L8::HALF);
         L8::quad(0, 1, fa, fb, acc);
+        if constexpr (IEPI)
+          if (ep) iepi(C1{}, C1{});
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -860,6 +939,8 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
         }
         pb0.issue(r + 2 - rb_off, bcur);
         pb1.issue(r + 2 - rb_off, bcur + L8::HALF);
+        if constexpr (IEPI)
+          if (ep) iepi(C1{}, C0{});
 #else
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
@@ -897,6 +978,20 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
           // the scan's 2 chunk-max stores of the previous tile stay in flight at r = 0
           if (r == 0 && epi_full) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
           else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else if (IEPI) {
+          // r = 0: the previous tile's stores (all quadrants, EPI_STORES) and K-tile 2's 8 DMAs
+          // are younger than K-tile 1; r = 1: only quadrant (1,0)'s stores (a quarter) and
+          // K-tile 3's DMAs are younger than K-tile 2. A partial previous tile issued fewer
+          // stores: vmcnt(8) then waits for more than needed, never less
+          if (r == 0 && epi_full) {
+            if constexpr (EPI_STORES<TO> == 16) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+          } else if (r == 1 && epi_full) {
+            if constexpr (EPI_STORES<TO> == 16) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+          } else {
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          }
         } else if ((r == 0 && epi_full) || loose) {
           if constexpr (EPI_STORES<TO> == 16) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
           else asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
@@ -917,6 +1012,12 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
         continue;
       }
       const bool full = cur_t.m0 + 256 <= g.M && cur_t.n0 + 256 <= g.N && g.vec_ok;
+      if constexpr (IEPI) {  // the epilogue runs in the next tile's first K-tile (or after the loop)
+        prev_t = cur_t;
+        have_prev = true;
+        epi_full = __builtin_amdgcn_readfirstlane((int)full) != 0;
+        continue;
+      }
       epi_direct<TO>(g, acc, static_cast<TO*>(g.c[cur_t.bi]), g.bias[cur_t.bi], cur_t.m0, cur_t.n0, wm, wn, full);
       epi_full = __builtin_amdgcn_readfirstlane((int)full) != 0;
       continue;
@@ -1028,6 +1129,14 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
     }
     if (late && qn < qend) __builtin_amdgcn_s_barrier();  // re-stagger for the next tile
   }
+  if constexpr (IE && A3 && !HN && PERSIST_BAL && std::is_same<TO, bf16_t>::value) {  // the last tile's epilogue
+    if (have_prev) {
+      iepi(C0{}, C0{});
+      iepi(C0{}, C1{});
+      iepi(C1{}, C1{});
+      iepi(C1{}, C0{});
+    }
+  }
   if constexpr (A3)
     if (!late) __builtin_amdgcn_s_barrier();  // the late row's extra prologue barrier
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing zero-page DMAs land before exit
@@ -1095,6 +1204,16 @@ int launch_persist(int akout, int bkout, bool shift, const GemmArgs& g0, int nti
     else TT_L(AK, BK, SH, false, false);   \
   } while (0)
   const bool a3 = tt::opt(tt::OPT_GEMM_A3) != 0;
+  // interleaved epilogue (gemm_persist IE): NT, bf16 out, full tiles, alpha 1, bias only
+  if constexpr (std::is_same<TO, bf16_t>::value) {
+    if (PERSIST_IEPI && tt::opt(tt::OPT_GEMM_IEPI) && !akout && !bkout && !shift && a3 && buf && g.M % 256 == 0 &&
+        g.N % 256 == 0 && g.vec_ok && g.bias_vec_ok && g.alpha == 1.f && !g.relu && !g.drop_thresh && !g.beta &&
+        g.stream_out <= 1 && g.force_regstage == 0) {
+      hipLaunchKernelGGL((gemm_persist<T, false, false, false, TO, true, true, false, true>), grid, blk, 0, st, g, ntiles);
+      TT_CHECK_LAUNCH("gemm_persist");
+      return 0;
+    }
+  }
   if (!akout && !bkout) TT_L2(false, false, false);
   else if (!akout && bkout && !shift) TT_L2(false, true, false);
   else if (!akout && bkout && shift) TT_L2(false, true, true);

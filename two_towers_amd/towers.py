@@ -406,6 +406,20 @@ def _gru_layer_bwd(cfg, layer, B, T, S, Y, dY, dfinal, packs):
 
 
 _WGRAD_T = os.environ.get("TT_WGRAD_T", "1") != "0"  # layer-0 dW_ih as its transpose (read once)
+# layer-1 weight gradients on a second stream, beside the layer-0 BPTT (see TowersFn.backward).
+# Off: measured slower -- sharing the CUs stretched the layer-0 BPTT from 5.9 to ~14 ms, so
+# 154.4-154.8k became 152.3-152.5k pairs/s (profiles/r06_wgrad_overlap_ab.txt)
+WGRAD_OVERLAP = os.environ.get("TT_WGRAD_OVERLAP", "0") == "1"
+_wgrad_streams: dict = {}
+
+
+def _wgrad_stream(dev) -> torch.cuda.Stream:
+    dev = torch.device(dev)
+    with _status_lock:
+        s = _wgrad_streams.get(dev)
+        if s is None:
+            s = _wgrad_streams[dev] = torch.cuda.Stream(device=dev)
+    return s
 
 
 def _weight_grads(cfg, B, T, dG, Xin, K, ldx, Y, kr=None):
@@ -561,14 +575,24 @@ class TowersFn(torch.autograd.Function):
         # ---- GRU layer 1: dfinal enters at the last processed step of each direction
         dG1, dbih1, dbhh1 = _gru_layer_bwd(cfg, 1, B, T, S1, Y1, None, dhcat, packs)
         Xl1 = X1 if X1 is not None else Y0
-        dWih1, dWhh1 = _weight_grads(cfg, B, T, dG1, Xl1, 2 * H, 2 * H, Y1)
-        gl = [{} for _ in range(n)]
-        _layer_grads(gl, 1, E, Ep, dWih1, dWhh1, dbih1, dbhh1)
-        # data-parallel: the head + layer-1 gradients are summed across ranks while the
-        # layer-0 BPTT below runs (dist.OverlapReducer)
         red = dist.OverlapReducer(ctx.group[0]) if ctx.group is not None else None
-        if red is not None:
-            _reduce_into(red, gl, head_grads)
+        gl = [{} for _ in range(n)]
+
+        def layer1_wgrads():
+            dWih1, dWhh1 = _weight_grads(cfg, B, T, dG1, Xl1, 2 * H, 2 * H, Y1)
+            _layer_grads(gl, 1, E, Ep, dWih1, dWhh1, dbih1, dbhh1)
+            # data-parallel: the head + layer-1 gradients are summed across ranks while the
+            # layer-0 BPTT below runs (dist.OverlapReducer)
+            if red is not None:
+                _reduce_into(red, gl, head_grads)
+
+        # The layer-1 weight gradients (MFMA-bound TN GEMMs) do not feed the layer-0 BPTT
+        # (HBM-bound, row-owning: no co-residency requirement), so with WGRAD_OVERLAP they run on
+        # a second stream beside it; the layer-1 data gradient, which the BPTT needs, goes first.
+        main = torch.cuda.current_stream(dev)
+        side = _wgrad_stream(dev) if WGRAD_OVERLAP else None
+        if side is None:
+            layer1_wgrads()
         # dL/dY0 = (dG1 Wih1) * dropout mask  [B*T, 2H]
         dY0 = [_alloc((B * T, 2 * H), dt, dev) for _ in range(n)]
         esz = 2 if dt == torch.bfloat16 else 4
@@ -582,6 +606,13 @@ class TowersFn(torch.autograd.Function):
                     ops.gemm([dG1[ti]], [packs[ti].wih[1]], [dY0[ti]], m=B * T, n=2 * H, k=6 * H, lda=8 * H,
                              ldb=2 * H, ldc=2 * H, a_kouter=False, b_kouter=True, dtype=dt, out_dtype=dt,
                              drop_seed=ctx.seeds[ti], drop_p=cfg.drop_p, drop_row0=cfg.rank * B * T)
+        if side is not None:
+            side.wait_stream(main)
+            for t in (*dG1, *Xl1, *Y1, *[g for hg in head_grads for g in hg], *[x for b in dbih1 for x in b],
+                      *[x for b in dbhh1 for x in b]):
+                t.record_stream(side)  # read on the side stream after main drops them
+            with torch.cuda.stream(side):
+                layer1_wgrads()
         del dG1
         # ---- GRU layer 0
         dG0, dbih0, dbhh0 = _gru_layer_bwd(cfg, 0, B, T, S0, Y0, dY0, None, packs)
@@ -589,6 +620,10 @@ class TowersFn(torch.autograd.Function):
         dWih0, dWhh0 = _weight_grads(cfg, B, T, dG0, X0, Ep, Ep, Y0, kr=E)
         gl0 = [{} for _ in range(n)]
         _layer_grads(gl0, 0, E, Ep, dWih0, dWhh0, dbih0, dbhh0)
+        if side is not None:
+            main.wait_stream(side)
+            for t in [*[v for d in gl for v in d.values()], *[g for hg in head_grads for g in hg]]:
+                t.record_stream(main)  # made on the side stream, used (and freed) on main
         if red is not None:
             _reduce_into(red, gl0, [[] for _ in range(n)])
             red.finish(ctx.params)

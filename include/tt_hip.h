@@ -43,8 +43,8 @@ const char* tt_last_error(void);
  * GRU: gru_step, gru_depth, gru_bwd_rows, gru_bwd_big, gru_bwd_streams, gru_bwd_persist,
  * gru_bwd_skew, gru_fwd_step_rows, gru_fwd_xc, gru_fwd_xs, gru_fwd_skew, gru_xc_coop,
  * gru_step_ring; GEMM: gemm_persist, gemm_persist_maxk, gemm_a3, gemm_buf, gemm_bres,
- * gemm_order, gemm_skew, gemm_regstage, gemm_stream_out; losses: hn_gemm, hn_map,
- * infonce_flash; diagnostics gru_xc_skip, gru_xc_spins. The authoritative list with
+ * bres_rows, gemm_iepi, gemm_order, gemm_skew, gemm_regstage, gemm_stream_out; losses:
+ * hn_gemm, hn_map, hn_scan_gemm, infonce_flash; diagnostics gru_xc_skip, gru_xc_spins. The authoritative list with
  * defaults is kOpts in two_towers_amd/csrc/tt_gemm.hip. Every variant computes the same
  * function; they exist for A/B measurement and for tests that compare variants.
  * Not synchronised with launches in flight: set them between steps. */

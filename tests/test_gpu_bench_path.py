@@ -3,7 +3,7 @@
 BASELINE configs[2] runs EnhancedTwoTowerModel(300, 256) (GRU H = 512 per direction),
 seq_len 64, bf16, dropout 0.1, hard-negative mining k = 5 + MarginRankingLoss(0.2).
 These tests run the kernels that step runs -- the column-split persistent GRU forward
-(gru_fwd_xcp<512, *>, which bench.py's B 8192 selects; forced here with option
+(gru_fwd_xs<512, *>, which bench.py's B 8192 selects; forced here with option
 gru_fwd_xc = 2 because its auto mode needs B >= 1024 and the oracle wants a small batch)
 and the row-owning one it falls back to (gru_fwd_seq<4, 8>, the auto choice at these
 batches), the row-owning BPTT kernel (gru_bwd_rows<512>, one launch per layer), the
@@ -75,7 +75,7 @@ def _grad_check(named, ref):
 
 def _xc_forced(xc):
     """option gru_fwd_xc: 1 = auto (row-owning gru_fwd_seq at these batches), 2 = the
-    column-split gru_fwd_xcp forced; asserts which one the shape gets."""
+    column-split gru_fwd_xs forced; asserts which one the shape gets."""
     lib = _lib.load()
     ws = lib.tt_gru_fwd_ws_size(_lib.DT_BF16, 4, B, T, 2 * HID, 6 * 2 * HID, 2 * 2 * HID)
     assert (ws > 0) == (xc == 2), (xc, ws)
@@ -194,7 +194,8 @@ def test_bench_composition_hardneg_margin_matches_oracle(xc):
     loss through the oracle's forward/backward (so a differing near-tie pick is not counted
     as a gradient error): loss relative 5e-3, tower outputs as above, gradients with the
     tolerances stated at the top of this file. xc 2: with the column-split forward bench.py
-    runs at B 8192 (gru_fwd_xcp), forced at this batch."""
+    runs at B 8192 (gru_fwd_xs), forced at this batch. The same step with nothing forced (B
+    1024): test_bench_b1024_unforced_kernel_selection_matches_oracle."""
     Bq, k = 512, 5
     m, p = _model(41)
     m.train()

@@ -229,9 +229,11 @@ def test_gemm_persistent_bf16_output_is_rounded_fp32(stream):
 
 @pytest.mark.parametrize("m,n,k,nb,with_bias", [(524288, 3072, 320, 2, True), (70000, 3072, 320, 2, True),
                                                 (65579, 1536, 96, 1, False), (40000, 384, 352, 2, True)])
-def test_gemm_b_resident_matches_persistent(m, n, k, nb, with_bias):
+@pytest.mark.parametrize("rows", [32, 64])
+def test_gemm_b_resident_matches_persistent(m, n, k, nb, with_bias, rows):
     """gemm_bres (the layer-0 input projection: each workgroup keeps a 192-column panel of
-    B in LDS, its waves walk 32-row A tiles with no barrier) against the persistent 256x256
+    B in LDS, its waves walk 32-row A tiles (8 waves) or 64-row tiles (4 waves, option
+    bres_rows 64) with no barrier) against the persistent 256x256
     kernel (option gemm_bres = 0) on the same operands: the same MFMA instruction, operand
     roles and k order, so every bf16 output must be identical. The bench shape (M = B*T
     = 524,288, N = 6H = 3072, K = Ep = 320, two towers) and shapes whose rows do not fill
@@ -246,7 +248,7 @@ def test_gemm_b_resident_matches_persistent(m, n, k, nb, with_bias):
     outs = []
     for br in (1, 0):
         C = [torch.full((m, n), float("nan"), device=DEV, dtype=dt) for _ in range(nb)]
-        with option("gemm_bres", br):
+        with option("gemm_bres", br), option("bres_rows", rows):
             ops.gemm(A, B, C, m=m, n=n, k=k, lda=k, ldb=k, ldc=n, a_kouter=False, b_kouter=False, dtype=dt,
                      out_dtype=dt, bias=bias, splits=1)
         torch.cuda.synchronize()

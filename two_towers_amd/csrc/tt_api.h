@@ -45,6 +45,7 @@ enum Opt {
   OPT_HN_SCAN_GEMM,     // 1: hard-negative scan on the persistent 256x256 GEMM with a chunk-max epilogue
                         // (bit-identical; measured slower: 44.8 vs 38.7 us at 8192^2 x 256); 0: hn_scan_kernel
   OPT_GEMM_IEPI,        // 1: the persistent GEMM's plain bf16 bias epilogue interleaved into the next tile's first K-tile
+  OPT_BRES_ROWS,        // gemm_bres rows per wave tile: 32 (8 waves) or 64 (4 waves, each B fragment read feeds 4 MFMAs)
   OPT_N
 };
 int opt(Opt o);

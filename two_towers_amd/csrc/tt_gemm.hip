@@ -42,7 +42,7 @@ constexpr OptDef kOpts[OPT_N] = {
     {"gru_xc_coop", "TT_GRU_XC_COOP", 0},         {"gemm_buf", "TT_GEMM_BUF", 1},
     {"gemm_order", "TT_GEMM_ORDER", 0},           {"gru_step_ring", "TT_GRU_STEP_RING", 4},
     {"gru_fwd_xs", "TT_GRU_FWD_XS", 1},           {"hn_scan_gemm", "TT_HN_SCAN_GEMM", 0},
-    {"gemm_iepi", "TT_GEMM_IEPI", 1},
+    {"gemm_iepi", "TT_GEMM_IEPI", 1},             {"bres_rows", "TT_BRES_ROWS", 32},
 };
 struct OptTable {
   std::atomic<int> v[OPT_N];
@@ -118,6 +118,9 @@ constexpr int BM = 128, BN = 128;  // tile of the register-staged / small path
 // 1-D grid in XCD-aware order (ttg::xcd_remap): ids enumerate (batch*split, m-tile,
 // n-tile) with the n-tile fastest, so the tiles of one A panel, and all tiles of one
 // split-K slice, share an XCD's L2.
+#ifndef TT_TAIL_SKIP  // 0: tail tiles' idle wave rows run their MFMAs (traffic experiment only)
+#define TT_TAIL_SKIP 1
+#endif
 using ttg::xcd_remap;
 #ifndef PERSIST_IEPI  // 1: gemm_persist (A3) runs each tile's epilogue inside the next tile's first K-tile
 #define PERSIST_IEPI 1
@@ -166,7 +169,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_kernel(GemmArgs g) {
 
   // 8-phase loop: a wave row whose 128 tile rows all lie past M skips its MFMAs (tail tiles)
   constexpr bool L8T = DMA && TBM == 256 && TBN == 256 && WGM == 2 && WGN == 4;
-  const bool mm = !L8T || __builtin_amdgcn_readfirstlane((int)(m0 + (int)(threadIdx.x >> 8) * 128 < g.M));
+  const bool mm = !L8T || !TT_TAIL_SKIP || __builtin_amdgcn_readfirstlane((int)(m0 + (int)(threadIdx.x >> 8) * 128 < g.M));
   auto lrun = [&](const auto& la, const auto& lb) {
     if constexpr (L8T) ML::run(la, lb, g.K, kt0, kt1, lds, acc, mm);
     else ML::run(la, lb, g.K, kt0, kt1, lds, acc);
@@ -551,20 +554,27 @@ TT_DEV void epi_chunkmax(const GemmArgs& g, const f32x4 (&acc)[8][4], int m0, in
 #ifndef BRES_PD  // gemm_bres A prefetch: 1 a whole tile ahead, 0 half a tile
 #define BRES_PD 1
 #endif
-#ifndef BRES_PAIR  // 1: gemm_bres stores whole 128-B lines (row_pair) -- slower, off
-#define BRES_PAIR 0
-#endif
 #ifndef BRES_STAG  // waves 4-7 start BRES_STAG x 64 cycles late (0: together)
 #define BRES_STAG 0
 #endif
 constexpr int BR_COLS = 192;  // B panel columns per workgroup
-template <int NKS>  // k-steps of 32
-__global__ __launch_bounds__(512, 1) void gemm_bres(GemmArgs g, int npan, int nbatch) {
+// RB: 16-row blocks per wave tile. RB 2 (32-row tiles, 8 waves): every 16-byte B fragment
+// read from LDS feeds 2 MFMAs, so the LDS read port (128 B/clk per CU) needs twice the
+// matrix pipe's time -- with neither stores nor A loads the kernel still took 1.60 ms per
+// step against 0.82 for its MFMAs alone (profiles/r05_bres_diag.txt). RB 4 (64-row tiles,
+// 4 waves of up to 512 registers, option bres_rows 64): each fragment feeds 4 MFMAs. Same
+// MFMAs per output element in the same k order either way: bit-identical.
+template <int NKS, int RB = 2>  // k-steps of 32
+__global__ __launch_bounds__(RB == 2 ? 512 : 256, 1) void gemm_bres(GemmArgs g, int npan, int nbatch) {
+  static_assert(RB == 2 || RB == 4, "32- or 64-row wave tiles");
+  constexpr int NW = RB == 2 ? 8 : 4;  // waves
+  constexpr int NT = 64 * NW;
+  constexpr int TR = 16 * RB;          // rows per wave tile
   constexpr int NKT = (NKS + 1) / 2;  // 64-deep K-tile images
   constexpr int IMG = BR_COLS * ttg::KTB;
   // A prefetch depth in k-steps (divides NKS); BRES_PD 1: a whole tile, so that the next
   // tile's fragments are all requested before this tile's stores (one in-order vmcnt)
-  constexpr int PD = ((BRES_PD && NKS <= 10) || NKS % 2 != 0) ? NKS : NKS / 2;  // (NKS 12: 20 spills)
+  constexpr int PD = ((BRES_PD && NKS * RB <= 20) || NKS % 2 != 0) ? NKS : NKS / 2;  // (NKS 12: 20 spills)
   __shared__ __attribute__((aligned(16))) char lds[NKT * IMG + BR_COLS * 4];
   float* bias_s = reinterpret_cast<float*>(lds + NKT * IMG);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -580,102 +590,67 @@ __global__ __launch_bounds__(512, 1) void gemm_bres(GemmArgs g, int npan, int nb
   bf16_t* C = static_cast<bf16_t*>(g.c[bi]);
   const float* bias = g.bias[bi];
   // the panel of B -> K-tile images (rows of 128 B, kc_off swizzle), zero past K; bias -> LDS
-  for (int id = tid; id < NKT * BR_COLS * 8; id += 512) {
+  for (int id = tid; id < NKT * BR_COLS * 8; id += NT) {
     const int kt = id / (BR_COLS * 8), rem = id % (BR_COLS * 8), row = rem >> 3, c = rem & 7;
     const int k = kt * 64 + c * 8;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (k < g.K) v = *reinterpret_cast<const uint4*>(Bm + (long)(n0 + row) * g.ldb + k);
     *reinterpret_cast<uint4*>(lds + kt * IMG + ttg::kc_off(row, c)) = v;
   }
-  for (int c = tid; c < BR_COLS; c += 512) bias_s[c] = bias ? bias[n0 + c] : 0.f;
+  for (int c = tid; c < BR_COLS; c += NT) bias_s[c] = bias ? bias[n0 + c] : 0.f;
   __syncthreads();
-  // this group's rows, in 32-row tiles dealt to the waves round-robin
-  const int mg = ((g.M + ngrp - 1) / ngrp + 31) / 32 * 32;
+  // this group's rows, in TR-row tiles dealt to the waves round-robin
+  const int mg = ((g.M + ngrp - 1) / ngrp + TR - 1) / TR * TR;
   const int g0 = gi * mg;
-  const int ntl = max(0, min(mg, g.M - g0) + 31) / 32;
+  const int ntl = max(0, min(mg, g.M - g0) + TR - 1) / TR;
   const __amdgpu_buffer_rsrc_t ra = tt_rsrc_n(A + (long)g0 * g.lda, g0 < g.M);
   const int lr = lane & 15, q = lane >> 4;
   // A fragment of (tile t, k-step ks, row block rb): rows past M read zero (offset past the
   // resource's range)
   auto lda_frag = [&](int t, int ks, int rb) {
-    const int row = t * 32 + rb * 16 + lr;
+    const int row = t * TR + rb * 16 + lr;
     const uint32_t off = t < ntl && g0 + row < g.M ? (uint32_t)((row * (int)g.lda + ks * 32 + q * 8) * 2) : 0x80000000u;
     return ld16_buf(ra, off, 0);
   };
-  if (BRES_STAG > 0 && wave >= 4) __builtin_amdgcn_s_sleep(BRES_STAG);
-  uint4 ar[PD][2];
+  if (BRES_STAG > 0 && wave >= NW / 2) __builtin_amdgcn_s_sleep(BRES_STAG);
+  uint4 ar[PD][RB];
   int t = wave;
 #pragma unroll
-  for (int i = 0; i < PD; ++i) {
-    ar[i][0] = lda_frag(t, i, 0);
-    ar[i][1] = lda_frag(t, i, 1);
-  }
-  for (; t < ntl; t += 8) {
-    f32x4 acc[2][BR_COLS / 16];
+  for (int i = 0; i < PD; ++i)
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
+    for (int rb = 0; rb < RB; ++rb) ar[i][rb] = lda_frag(t, i, rb);
+  for (; t < ntl; t += NW) {
+    f32x4 acc[RB][BR_COLS / 16];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int j = 0; j < BR_COLS / 16; ++j) acc[rb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
-      const uint4 a0 = ar[ks % PD][0], a1 = ar[ks % PD][1];
+      uint4 a[RB];
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) a[rb] = ar[ks % PD][rb];
       // refill the slot: k-step ks + PD of this tile, or of the wave's next tile
-      if (ks + PD < NKS) {
-        ar[ks % PD][0] = lda_frag(t, ks + PD, 0);
-        ar[ks % PD][1] = lda_frag(t, ks + PD, 1);
-      } else {
-        ar[ks % PD][0] = lda_frag(t + 8, ks + PD - NKS, 0);
-        ar[ks % PD][1] = lda_frag(t + 8, ks + PD - NKS, 1);
-      }
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+        ar[ks % PD][rb] = ks + PD < NKS ? lda_frag(t, ks + PD, rb) : lda_frag(t + NW, ks + PD - NKS, rb);
       const char* img = lds + (ks >> 1) * IMG;
 #pragma unroll
       for (int j = 0; j < BR_COLS / 16; ++j) {
         const uint4 fb = ttg::frag<bf16_t, false>(img, 16 * j, ks & 1);
-        acc[0][j] = ttg::mma<bf16_t>(fb, a0, acc[0][j]);
-        acc[1][j] = ttg::mma<bf16_t>(fb, a1, acc[1][j]);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) acc[rb][j] = ttg::mma<bf16_t>(fb, a[rb], acc[rb][j]);
       }
       // one k-step per scheduling region: hipcc would otherwise hoist every B fragment
       // read of the tile ahead of the MFMAs (and spill)
       __builtin_amdgcn_sched_barrier(0);
     }
-    // epilogue: acc[rb][j][e] = C(row 32t + 16rb + lr, col 16j + 4q + e); bias, bf16, pairs of
+    // epilogue: acc[rb][j][e] = C(row TR t + 16rb + lr, col 16j + 4q + e); bias, bf16, pairs of
     // column tiles exchanged (v_permlane16_swap) into 16-byte row stores
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb) {
-      const int row = t * 32 + rb * 16 + lr;
+    for (int rb = 0; rb < RB; ++rb) {
+      const int row = t * TR + rb * 16 + lr;
       const bool ok = g0 + row < g.M;
-#if BRES_PAIR && !(BRES_DIAG & 1) && BRES_STORE == 0  // measured slower: 3.33 vs 2.89 ms (profiles/r06_epi_pair_ab.txt)
-      if (g0 + t * 32 + rb * 16 + 16 <= g.M) {  // whole 128-B lines: 8 rows per store (row_pair)
-#pragma unroll
-        for (int a = 0; a < BR_COLS / 64; ++a) {
-          uint4 v[2];
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const int jp = 2 * a + u;
-            uint32_t w[2][2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const int j = 2 * jp + h;
-              const float4 b4 = *reinterpret_cast<const float4*>(bias_s + 16 * j + 4 * q);
-              const float v0 = acc[rb][j][0] + b4.x, v1 = acc[rb][j][1] + b4.y;
-              const float v2 = acc[rb][j][2] + b4.z, v3 = acc[rb][j][3] + b4.w;
-              w[h][0] = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
-              w[h][1] = (uint32_t)f2bf(v2) | ((uint32_t)f2bf(v3) << 16);
-            }
-            const auto s0 = __builtin_amdgcn_permlane16_swap(w[0][0], w[1][0], false, false);
-            const auto s1 = __builtin_amdgcn_permlane16_swap(w[0][1], w[1][1], false, false);
-            v[u] = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-          }
-          uint4 da, db;
-          row_pair(v[0], v[1], da, db);
-          const long ra = g0 + t * 32 + rb * 16 + (lr & 7);
-          const int cs = n0 + 64 * a + 16 * (q & 1) + 8 * (q >> 1) + (lr & 8 ? 32 : 0);
-          *reinterpret_cast<uint4*>(C + ra * g.ldc + cs) = da;
-          *reinterpret_cast<uint4*>(C + (ra + 8) * g.ldc + cs) = db;
-        }
-        continue;
-      }
-#endif
 #pragma unroll
       for (int jp = 0; jp < BR_COLS / 32; ++jp) {
         uint32_t w[2][2];
@@ -1142,24 +1117,42 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing zero-page DMAs land before exit
 }
 
-// out_b[m][n] = alpha * sum_s part_b[s][m][n] (+ bias[n]) (+ out_b)
-template <typename TO>
+// out_b[m][n] = alpha * sum_s part_b[s][m][n] (+ bias[n]) (+ out_b); V consecutive elements
+// of one row per thread (V 4: N % 4 == 0, 16-byte partial loads), the slices summed in order
+// s = 0, 1, ... either way
+template <typename TO, int V>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* ws, long part_stride, int splits,
                                                             int M, int N, GemmArgs g) {
   const int bi = blockIdx.y;
   const float* P = ws + (long)bi * splits * part_stride;
   TO* C = static_cast<TO*>(g.c[bi]);
   const float* bias = g.bias[bi];
-  const long total = (long)M * N;
+  const long total = (long)M * N / V;
   for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
-    float v = 0.f;
-    for (int s = 0; s < splits; ++s) v += P[(long)s * part_stride + e];
-    const int m = (int)(e / N), n = (int)(e % N);
-    v *= g.alpha;
-    if (bias) v += bias[n];
-    TO* p = C + (long)m * g.ldc + n;
-    if (g.beta) v += Elt<TO>::ld(p);
-    Elt<TO>::st(p, v);
+    float v[V];
+    if constexpr (V == 4) {
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int s = 0; s < splits; ++s) {
+        const float4 b = reinterpret_cast<const float4*>(P + (long)s * part_stride)[e];
+        a.x += b.x;
+        a.y += b.y;
+        a.z += b.z;
+        a.w += b.w;
+      }
+      v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w;
+    } else {
+      v[0] = 0.f;
+      for (int s = 0; s < splits; ++s) v[0] += P[(long)s * part_stride + e];
+    }
+    const int m = (int)(e * V / N), n0 = (int)(e * V % N);
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      float x = v[u] * g.alpha;
+      if (bias) x += bias[n0 + u];
+      TO* p = C + (long)m * g.ldc + n0 + u;
+      if (g.beta) x += Elt<TO>::ld(p);
+      Elt<TO>::st(p, x);
+    }
   }
 }
 
@@ -1242,9 +1235,16 @@ bool try_bres(int akout, int bkout, bool shift, const GemmArgs& g, int nbatch, h
     const int npan = g.N / BR_COLS, ptot = npan * nbatch, nwg = 256;
     if (ptot > nwg || nwg % ptot) return false;
     if ((long)g.M < (long)(nwg / ptot) * 256 || (long)g.M * g.lda * 2 >= (1L << 31)) return false;
-    const dim3 grid(nwg), blk(512);
+    const bool r64 = tt::opt(tt::OPT_BRES_ROWS) == 64;
+    const dim3 grid(nwg), blk(r64 ? 256 : 512);
     switch (g.K / 32) {
-#define TT_BR(n) case n: hipLaunchKernelGGL(gemm_bres<n>, grid, blk, 0, st, g, npan, nbatch); break;
+#define TT_BR(n)                                                                   \
+  case n:                                                                          \
+    if (r64)                                                                       \
+      hipLaunchKernelGGL((gemm_bres<n, 4>), grid, blk, 0, st, g, npan, nbatch);    \
+    else                                                                           \
+      hipLaunchKernelGGL((gemm_bres<n, 2>), grid, blk, 0, st, g, npan, nbatch);    \
+    break;
       TT_BR(1) TT_BR(2) TT_BR(3) TT_BR(4) TT_BR(5) TT_BR(6) TT_BR(7) TT_BR(8) TT_BR(9) TT_BR(10) TT_BR(11) TT_BR(12)
 #undef TT_BR
       default: return false;
@@ -1446,12 +1446,16 @@ extern "C" int tt_gemm(int dtype, int out_dtype, int a_kouter, int b_kouter, int
     int rc = dtype == TT_DT_BF16 ? launch_gemm<bf16_t, float>(a_kouter, b_kouter, shift, gp, nbatch, st)
                                  : launch_gemm<float, float>(a_kouter, b_kouter, shift, gp, nbatch, st);
     if (rc) return rc;
-    const long total = (long)m * n;
+    const bool v4 = n % 4 == 0 && (uintptr_t)splitk_ws % 16 == 0;  // dense [m][n] partials, 16-byte rows
+    const long total = (long)m * n / (v4 ? 4 : 1);
     dim3 rg((unsigned)std::min<long>(tt_ceil_div(total, 256), 2048), nbatch);
-    if (out_dtype == TT_DT_F32)
-      hipLaunchKernelGGL(splitk_reduce_kernel<float>, rg, dim3(256), 0, st, splitk_ws, gp.part_stride, splits, m, n, g);
-    else
-      hipLaunchKernelGGL(splitk_reduce_kernel<bf16_t>, rg, dim3(256), 0, st, splitk_ws, gp.part_stride, splits, m, n, g);
+#define TT_RED(TO, V) hipLaunchKernelGGL((splitk_reduce_kernel<TO, V>), rg, dim3(256), 0, st, splitk_ws, gp.part_stride, splits, m, n, g)
+    if (out_dtype == TT_DT_F32) {
+      if (v4) TT_RED(float, 4); else TT_RED(float, 1);
+    } else {
+      if (v4) TT_RED(bf16_t, 4); else TT_RED(bf16_t, 1);
+    }
+#undef TT_RED
     TT_CHECK_LAUNCH("splitk_reduce_kernel");
     return 0;
   }

@@ -1372,9 +1372,9 @@ typedef __attribute__((address_space(1))) unsigned xc_gu32;
 #ifndef XC_G_AUX  // cache policy of the column-split forward's G loads (2: non-temporal, measured 2% faster)
 #define XC_G_AUX 2
 #endif
-#ifndef XC_OUT_AUX
-#define XC_OUT_AUX 0
-#endif
+#ifndef XC_OUT_AUX  // cache policy of the column-split forward's Y / S / X1 stores (2: non-temporal):
+#define XC_OUT_AUX 2  // plain stores evicted the group's h images from L2 before the members read them
+#endif                // (fetch 8.61 -> 6.52 GB per launch, 9.70 -> 9.65 ms per step; profiles/r06_xs_out_policy_ab.txt)
 #ifndef XC_VALU_PER_MFMA
 #define XC_VALU_PER_MFMA 3
 #endif

@@ -161,12 +161,37 @@ def test_hardneg_scan_gemm_matches_scan_kernel(B, nd, h, lab, k):
     assert float((gv.double() - rv).abs().max()) < 1e-5  # fp32 accumulation of bf16 products
 
 
+@pytest.mark.parametrize("B,nd,lab", [(8192, 8192, 0), (8192, 65536, 8192), (1000, 3000, 0), (513, 4100, 7),
+                                      (40, 70, 3)])
+def test_hardneg_scan_variants_match(B, nd, lab):
+    """The h 256 scan's variants (option hn_scan_v: 5 the five-slot ring with the chunk maxima
+    stored straight from registers, the default; 0 the round-3 form with the maxima staged in
+    LDS; 4 64 queries per wave) under each block map: the same MFMA sequence per score, so the
+    chunk maxima (masked positive and tail columns included) and the top-k are bit-identical.
+    Shapes: the bench's 8192^2, the configs[3] per-rank pool (8192 x 65,536, labels at the
+    rank's offset), ragged row tiles, partial chunks, fewer tiles than the ring's depth."""
+    g = torch.Generator().manual_seed(B + nd + lab)
+    q = torch.nn.functional.normalize(torch.randn(B, 256, generator=g), dim=1)
+    d = torch.nn.functional.normalize(torch.randn(nd, 256, generator=g), dim=1)
+    outs = {}
+    with option("hn_scan_gemm", 0):
+        for v in (5, 0, 4):
+            for m in (0, 2):
+                with option("hn_scan_v", v), option("hn_map", m):
+                    outs[(v, m)] = _scan_with_cm(q, d, lab, 5)
+    ri, rv, rcm = outs[(5, 2)]
+    for key, (i, val, cm) in outs.items():
+        assert torch.equal(rcm.view(torch.int32), cm.view(torch.int32)), (key, int((rcm != cm).sum()))
+        assert torch.equal(ri, i) and torch.equal(rv, val), key
+
+
 @pytest.mark.parametrize("B,nd,lab", [(8192, 8192, 0), (2048, 16384, 100), (1000, 3000, 0)])
-@pytest.mark.parametrize("hn_map", [1, 2])
+@pytest.mark.parametrize("hn_map", [0, 1, 2])
 def test_hardneg_scan_block_maps_agree(B, nd, lab, hn_map):
     """The scan's workgroup -> (row tile, document split) maps (option hn_map: 0 a split
-    per XCD, 1 a row tile per XCD, 2 row-tile halves x split quarters per XCD; 2 falls back
-    to 0 where the grid does not divide) only move work between workgroups: bit-identical."""
+    per XCD, 1 a row tile per XCD, 2 row-tile halves x split quarters per XCD, the default;
+    2 falls back to 0 where the grid does not divide) only move work between workgroups:
+    bit-identical."""
     g = torch.Generator().manual_seed(B + nd + hn_map)
     q = torch.nn.functional.normalize(torch.randn(B, 256, generator=g), dim=1)
     d = torch.nn.functional.normalize(torch.randn(nd, 256, generator=g), dim=1)

@@ -26,7 +26,7 @@ enum Opt {
   OPT_GRU_BWD_PERSIST,  // 0: per-step backward launches instead of the row-owning kernel; 2: also at H 1024
   OPT_GRU_FWD_STEP_ROWS, // per-step GRU forward batch rows per tile: 128, 256 (0: by size)
   OPT_INFONCE_FLASH,    // 0: InfoNCE backward through a materialised dS (bf16, h 128/256 default fused)
-  OPT_HN_MAP,           // hn_scan block -> (row tile, split) map: 0 split per XCD, 1 row tile per XCD
+  OPT_HN_MAP,           // hn_scan block -> (row tile, split) map: 0 split per XCD, 1 row tile per XCD, 2 (default) row-tile half x split quarter per XCD
   OPT_GEMM_SKEW,        // persistent GEMM: start workgroup w after (w % 4) * skew * 4096 cycles
   OPT_GEMM_PERSIST_MAXK,  // persistent GEMM for problems of at most this many K-tiles
   OPT_GRU_FWD_XC,       // column-split persistent forward: 0 off, 1 where the batch fills it, 2 wherever it
@@ -46,6 +46,7 @@ enum Opt {
                         // (bit-identical; measured slower: 44.8 vs 38.7 us at 8192^2 x 256); 0: hn_scan_kernel
   OPT_GEMM_IEPI,        // 1: the persistent GEMM's plain bf16 bias epilogue interleaved into the next tile's first K-tile
   OPT_BRES_ROWS,        // gemm_bres rows per wave tile: 32 (8 waves) or 64 (4 waves, each B fragment read feeds 4 MFMAs)
+  OPT_HN_SCAN_V,        // h 256 hard-negative scan variant: 0 round-3 form, 4 64 queries per wave, 5 five-slot ring
   OPT_N
 };
 int opt(Opt o);

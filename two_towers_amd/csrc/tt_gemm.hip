@@ -34,7 +34,7 @@ constexpr OptDef kOpts[OPT_N] = {
     {"gemm_a3", "TT_GEMM_A3", 1},                 {"gemm_regstage", "TT_GEMM_REGSTAGE", 0},
     {"gemm_stream_out", "TT_GEMM_STREAM_OUT", 1}, {"hn_gemm", "TT_HN_GEMM", 0},
     {"gru_bwd_persist", "TT_GRU_BWD_PERSIST", 1}, {"gru_fwd_step_rows", "TT_GRU_FWD_STEP_ROWS", 0},
-    {"infonce_flash", "TT_INFONCE_FLASH", 1},     {"hn_map", "TT_HN_MAP", 0},
+    {"infonce_flash", "TT_INFONCE_FLASH", 1},     {"hn_map", "TT_HN_MAP", 2},
     {"gemm_skew", "TT_GEMM_SKEW", 0},             {"gemm_persist_maxk", "TT_GEMM_PERSIST_MAXK", 24},
     {"gru_fwd_xc", "TT_GRU_FWD_XC", 1},           {"gru_xc_skip", "TT_GRU_XC_SKIP", 0},
     {"gru_xc_spins", "TT_GRU_XC_SPINS", 22},      {"gru_bwd_skew", "TT_GRU_BWD_SKEW", 14},
@@ -43,6 +43,7 @@ constexpr OptDef kOpts[OPT_N] = {
     {"gemm_order", "TT_GEMM_ORDER", 0},           {"gru_step_ring", "TT_GRU_STEP_RING", 4},
     {"gru_fwd_xs", "TT_GRU_FWD_XS", 1},           {"hn_scan_gemm", "TT_HN_SCAN_GEMM", 0},
     {"gemm_iepi", "TT_GEMM_IEPI", 1},             {"bres_rows", "TT_BRES_ROWS", 32},
+    {"hn_scan_v", "TT_HN_SCAN_V", 5},
 };
 struct OptTable {
   std::atomic<int> v[OPT_N];

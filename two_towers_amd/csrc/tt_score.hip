@@ -35,6 +35,9 @@ namespace {
 #ifndef HN_DSPLIT  // h 256: 1 = every wave takes all 64 documents of a tile for 32 queries (the
 #define HN_DSPLIT 1  // round-3 form, 37.7 us); 2 = half the documents for 64 queries (41.9 us, r05_hn_scan_ab)
 #endif
+#ifndef HN_Q64_PF  // fragment prefetch distance (k-steps) of the 64-query scan: 0 keeps it spill-free
+#define HN_Q64_PF 0
+#endif
 constexpr int SC_COLS = 64;     // document columns per tile (= per chunk)
 constexpr int SC_TPS_MAX = 32;  // tiles per workgroup (chunk-max staging)
 
@@ -48,15 +51,32 @@ constexpr int SC_TPS_MAX = 32;  // tiles per workgroup (chunk-max staging)
 // each tile from LDS 4 times instead of 8 -- the LDS reads, not the MFMAs, were the
 // largest part of the scan (profiles/r04_hn_scan_diag.txt: 11 of 38 us). The two
 // halves' chunk maxima meet in LDS (ds_max_f32; max is exact in any order).
-template <int KS>
+// V: the variant (option hn_scan_v; h 256 only, 0 elsewhere).
+// V 4: 8 waves of 64 queries (4 MFMA blocks) x all 64 documents of a tile, 512 query rows
+// per workgroup: every LDS fragment read feeds 4 MFMAs (the workgroup reads a tile from
+// LDS once per 64 queries instead of once per 32) and a workgroup's 512 x (8 tiles) block
+// needs 512 KiB into the CU instead of 640; single accumulator set (the partner wave on the
+// SIMD covers each wave's chunk-max epilogue), chunk maxima of at most 8 tiles staged.
+// V 5: the round-3 body on a 5-slot ring retired ONE tile per barrier, four tiles (128 KiB)
+// in flight instead of one pair (64 KiB): the chunk maxima leave the LDS (each wave stores
+// its rows' maxima straight to CM, 16 lanes x 4 B per query block and tile) to make room,
+// and every wait is counted (vmcnt = the DMAs of the 3 younger tiles + the 4 younger tiles'
+// maxima stores; every tile issues the same DMA and store count, past-the-end tiles read
+// the zero page or the next split's documents into a free slot).
+template <int KS, int V = 0>
 struct ScanCfg {
   static constexpr int WAVES = KS <= 8 ? 8 : 4;
-  static constexpr int DH = KS == 8 ? HN_DSPLIT : 1;  // document splits per tile
-  static constexpr int RB = 2 * DH;                   // 16-query MFMA blocks per wave
-  static constexpr int NDB = 4 / DH;                  // 16-document blocks per wave
-  static constexpr int QW = WAVES / DH;               // query groups
+  static constexpr int DH = KS == 8 && V == 0 ? HN_DSPLIT : 1;  // document splits per tile
+  static constexpr int RB = V == 4 ? 4 : 2 * DH;                 // 16-query MFMA blocks per wave
+  static constexpr int NDB = 4 / DH;                             // 16-document blocks per wave
+  static constexpr int QW = WAVES / DH;                          // query groups
   static constexpr int ROWS = QW * RB * 16;
-  static constexpr int SLOTS = KS <= 8 ? 4 : 2;
+  static constexpr int SLOTS = V == 5 ? 5 : KS <= 8 ? 4 : 2;
+  static constexpr bool SINGLE = DH > 1 || V == 4;  // one accumulator set, maxima after each tile
+  static constexpr bool DIRECT = V == 5;            // maxima stored to CM from registers
+  static constexpr int TPSM = V == 4 ? 8 : V == 5 ? 0 : SC_TPS_MAX;  // chunk-max staging (tiles)
+  static constexpr long PLAN_TPS = V == 5 ? (1L << 30) : TPSM;       // tiles per workgroup cap
+  static constexpr int PF = V == 4 ? HN_Q64_PF : 2;                  // fragment prefetch, k-steps ahead
 };
 
 // max over the four 16-lane rows of a wave (lanes l, l+16, l+32, l+48), result in all
@@ -81,25 +101,34 @@ struct ScanTile {
 
 // One lane's share of a tile DMA, resolved once: element offset within the tile and the
 // tile document it reads.
-template <int KS>
+template <int KS, bool LAZY = false>  // LAZY: the lane's (document, offset) recomputed per piece (no registers held)
 struct ScanDma {
   using TI = ScanTile<KS>;
-  int doc[TI::DPW];
-  int eoff[TI::DPW];
-  TT_DEV void init() {
+  int doc[LAZY ? 1 : TI::DPW];
+  int eoff[LAZY ? 1 : TI::DPW];
+  TT_DEV static void at(int i, int& n, int& e) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int p = (wave * TI::DPW + i) * 64 + lane;
+    n = p / TI::CPR;
+    e = n * (32 * KS) + ((p % TI::CPR) ^ (n & 15)) * 8;
+  }
+  TT_DEV void init() {
+    if constexpr (!LAZY) {
 #pragma unroll
-    for (int i = 0; i < TI::DPW; ++i) {
-      const int p = (wave * TI::DPW + i) * 64 + lane;
-      const int n = p / TI::CPR, c = (p % TI::CPR) ^ (n & 15);
-      doc[i] = n;
-      eoff[i] = n * (32 * KS) + c * 8;
+      for (int i = 0; i < TI::DPW; ++i) at(i, doc[i], eoff[i]);
     }
   }
   // piece i of the tile starting at document n0 into the slot at LDS address base
   TT_DEV void piece(const bf16_t* __restrict__ D, long nd, long n0, uint32_t base, int i) const {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const void* src = n0 + doc[i] < nd ? static_cast<const void*>(D + n0 * (32 * KS) + eoff[i]) : ttg::g_tt_zero_page;
+    int n, e;
+    if constexpr (LAZY) {
+      at(i, n, e);
+    } else {
+      n = doc[i];
+      e = eoff[i];
+    }
+    const void* src = n0 + n < nd ? static_cast<const void*>(D + n0 * (32 * KS) + e) : ttg::g_tt_zero_page;
     ttg::dma16(src, __builtin_amdgcn_readfirstlane(base + (uint32_t)(wave * TI::DPW + i) * 1024u));
   }
   TT_DEV void issue(const bf16_t* __restrict__ D, long nd, long n0, uint32_t base) const {
@@ -122,17 +151,18 @@ TT_DEV uint4 ld_frag(const bf16_t* __restrict__ base, long row, long nrows, int 
 // 64-document tile and the chunk maximum is 15 lane-local max + two permlane swaps.
 // Grid: row tiles x column splits, 1-D: block b -> split b % S (a split's workgroups
 // share one XCD label and its document slice stays in that L2), row tile b / S.
-template <int KS>
+template <int KS, int V = 0>
 __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(const bf16_t* __restrict__ Q, long bq,
                                                                  const bf16_t* __restrict__ D, long nd,
                                                                  long label_off, int S, int tps, long nch,
                                                                  float* __restrict__ CM, int map) {
   using TI = ScanTile<KS>;
-  constexpr int SC_WAVES = ScanCfg<KS>::WAVES, SC_ROWS = ScanCfg<KS>::ROWS, SC_SLOTS = ScanCfg<KS>::SLOTS;
-  constexpr int SC_RB = ScanCfg<KS>::RB, NDB = ScanCfg<KS>::NDB, DH = ScanCfg<KS>::DH, QW = ScanCfg<KS>::QW;
+  using Cfg = ScanCfg<KS, V>;
+  constexpr int SC_WAVES = Cfg::WAVES, SC_ROWS = Cfg::ROWS, SC_SLOTS = Cfg::SLOTS;
+  constexpr int SC_RB = Cfg::RB, NDB = Cfg::NDB, DH = Cfg::DH, QW = Cfg::QW, TPSM = Cfg::TPSM;
   // tile ring + chunk maxima [tile][row]: 4 x 32 KiB + 32 KiB (h 256) or 2 x 64 KiB + 16
   // KiB (h 512), one workgroup per CU
-  __shared__ __attribute__((aligned(16))) char lds[SC_SLOTS * TI::BYTES + SC_TPS_MAX * SC_ROWS * 4];
+  __shared__ __attribute__((aligned(16))) char lds[SC_SLOTS * TI::BYTES + TPSM * SC_ROWS * 4];
   float* cms = reinterpret_cast<float*>(lds + SC_SLOTS * TI::BYTES);
   // map 0: blocks round-robin over the XCDs, so split b % S stays on one XCD and its
   // document slice in that L2; map 1 (option hn_map): the S splits of a row tile share an
@@ -159,16 +189,20 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
   const long row0 = (long)rt * SC_ROWS + qw * (SC_RB * 16);
   if (DH > 1) {  // the halves' chunk maxima meet in LDS: start from -inf (ordered before
     // the first ds_max by tile 0's barrier)
-    for (int e = threadIdx.x; e < SC_TPS_MAX * SC_ROWS; e += SC_WAVES * 64) cms[e] = -FLT_MAX;
+    for (int e = threadIdx.x; e < TPSM * SC_ROWS; e += SC_WAVES * 64) cms[e] = -FLT_MAX;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
   constexpr int h = 32 * KS;
   // The first two tiles are requested before the query rows, so their latency overlaps.
-  ScanDma<KS> dm;
+  ScanDma<KS, (V == 4)> dm;
   dm.init();
   const uint32_t lbase = __builtin_amdgcn_readfirstlane(ttg::lds_addr_of(lds));
   dm.issue(D, nd, t0 * SC_COLS, lbase);
   if (SC_SLOTS == 4 && nt > 1) dm.issue(D, nd, (t0 + 1) * SC_COLS, lbase + TI::BYTES);
+  if constexpr (Cfg::DIRECT) {  // tiles 1-3 (unconditionally: uniform counts)
+#pragma unroll
+    for (int j = 1; j < 4; ++j) dm.issue(D, nd, (t0 + j) * SC_COLS, lbase + (uint32_t)j * TI::BYTES);
+  }
   uint4 qa[SC_RB][KS];
 #pragma unroll
   for (int qb = 0; qb < SC_RB; ++qb)
@@ -181,6 +215,10 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
       asm volatile("" ::"v"(qa[qb][ks].x), "v"(qa[qb][ks].y), "v"(qa[qb][ks].z), "v"(qa[qb][ks].w));
+  if constexpr (Cfg::DIRECT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tiles 0-3 landed
+  // CM rows of this workgroup through a buffer range: rows past bq store nothing (an
+  // offset past num_records), so every wave issues the same number of store instructions
+  const __amdgpu_buffer_rsrc_t rcm = tt_rsrc(CM);
 
   // Tiles travel in pairs: at every even tile, one wait + barrier retires the pair (t, t+1)
   // for every wave and frees slots (t+2)%4, (t+3)%4 (last read before this barrier), into
@@ -190,10 +228,19 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
   // The DMAs of the tiles that become due at tile t's barrier (t + 1 with two slots; t + 2
   // and t + 3 at the start of a pair) are issued at tile t's first k-step (HN_SPREAD 1:
   // spread over its k-steps, NPK per k-step -- slower, profiles/r05_hn_scan_ab_e.txt).
-  constexpr int NPD = SC_SLOTS == 2 ? TI::DPW : 2 * TI::DPW;  // pieces due per DMA tile
+  constexpr int NPD = SC_SLOTS == 4 ? 2 * TI::DPW : TI::DPW;  // pieces due per DMA tile
   constexpr int NPK = HN_SPREAD ? (NPD + KS - 1) / KS : NPD;  // pieces per k-step (0: all at k-step 0)
+  // 5-slot ring: tile t's DMAs were issued during tile t-4; younger than them: the DMAs of
+  // tiles t+1..t+3 and the maxima stores of tiles t-5..t-2 (issued while processing tiles
+  // t-4..t-1; tile 0 stores nothing during tile 0), SC_RB per tile
+  constexpr int VM_FULL = 3 * TI::DPW + 4 * SC_RB, VM_T4 = 3 * TI::DPW + 3 * SC_RB;
+  static_assert(!Cfg::DIRECT || VM_FULL < 64, "vmcnt range");
   auto sync = [&](int t) {
-    if (SC_SLOTS == 2 || (t & 1) == 0) {
+    if constexpr (Cfg::DIRECT) {
+      if (t == 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_T4) : "memory");
+      else if (t > 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_FULL) : "memory");
+      __builtin_amdgcn_s_barrier();  // every wave done with tile t-1: its slot takes tile t+4
+    } else if (SC_SLOTS == 2 || (t & 1) == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     }
@@ -205,7 +252,10 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
     for (int u = 0; u < NPK; ++u) {
       const int i = ks * NPK + u;
       if (i >= NPD) break;
-      if (SC_SLOTS == 2) {
+      if constexpr (Cfg::DIRECT) {
+        const int tt = t + 4;  // always issued (see sync)
+        dm.piece(D, nd, (t0 + tt) * SC_COLS, lbase + (uint32_t)(tt % 5) * TI::BYTES, i);
+      } else if (SC_SLOTS == 2) {
         if (t + 1 < nt) dm.piece(D, nd, (t0 + t + 1) * SC_COLS, lbase + (uint32_t)((t + 1) % 2) * TI::BYTES, i);
       } else if ((t & 1) == 0) {
         const int tt = t + 2 + i / TI::DPW;
@@ -218,6 +268,12 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
   // part's (ds_max_f32 on the -inf initialised slot)
   auto put_max = [&](int t, int qb, float m) {
     if (lane < 16) {
+      if constexpr (Cfg::DIRECT) {
+        const long row = row0 + qb * 16 + lane;
+        const uint32_t off = row < bq ? (uint32_t)((row * nch + t0 + t) * 4) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(m), rcm, (int)off, 0, 0);
+        return;
+      }
       float* dst = cms + t * SC_ROWS + qw * SC_RB * 16 + qb * 16 + lane;
       if constexpr (DH == 1) {
         *dst = m;
@@ -238,15 +294,18 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[db * 4 + r] = a[db][qb][r];
       if (masked) {
-        const int lab = (int)(label_off + row0) + qb * 16 + (lane & 15) - n0;  // tile-relative
-        const int lim = (int)(nd - n0);
+        // lane-relative: document (db0 + db) * 16 + 4 (lane >> 4) + r is the label iff
+        // db * 16 + r == lab, past nd iff db * 16 + r >= lim (compile-time left sides, so no
+        // per-element index registers are held across the tile loop)
+        const int sh = db0 * 16 + 4 * (lane >> 4) + (int)n0;
+        const int lab = (int)(label_off + row0) + qb * 16 + (lane & 15) - sh;
+        const int lim = (int)(nd - sh);
 #pragma unroll
         for (int db = 0; db < NDB; ++db)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int doc = (db0 + db) * 16 + 4 * (lane >> 4) + r;
-            if (diag && doc == lab) v[db * 4 + r] = -1.f;
-            if (doc >= lim) v[db * 4 + r] = -FLT_MAX;
+            if (diag && db * 16 + r == lab) v[db * 4 + r] = -1.f;
+            if (db * 16 + r >= lim) v[db * 4 + r] = -FLT_MAX;
           }
       }
       float m = fmaxf(fmaxf(v[0], v[1]), v[2]);
@@ -268,7 +327,7 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
 #pragma unroll
       for (int qb = 0; qb < SC_RB; ++qb) acc[db][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
     // fragment ring: k-steps PF ahead
-    constexpr int PF = 2;
+    constexpr int PF = Cfg::PF;
     uint4 fa[PF + 1][NDB];
 #pragma unroll
     for (int ks = 0; ks < PF; ++ks)
@@ -332,10 +391,10 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
       tile(cur, prev, t, true);
     }
   };
-  if constexpr (DH > 1) {
-    // document-split form: the 64-query fragments leave no registers for a second
-    // accumulator set, so each tile's maxima follow its own MFMAs (the partner wave on the
-    // SIMD keeps the matrix pipe busy meanwhile)
+  if constexpr (Cfg::SINGLE) {
+    // document-split and 64-query forms: the 64-query fragments leave no registers for a
+    // second accumulator set, so each tile's maxima follow its own MFMAs (the partner wave
+    // on the SIMD keeps the matrix pipe busy meanwhile)
     for (int t = 0; t < nt; ++t) {
       sync(t);
       tile(accA, accA, t, false);
@@ -355,6 +414,10 @@ __global__ __launch_bounds__(ScanCfg<KS>::WAVES * 64, 1) void hn_scan_kernel(con
     } else {
       chunk_max(accB, t - 1, special(t - 1));
     }
+  }
+  if constexpr (Cfg::DIRECT) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing zero-page / next-split DMAs land before exit
+    return;
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's ds_max (inline asm: not counted by hipcc)
   __syncthreads();
@@ -526,12 +589,12 @@ struct HnPlan {
 
 long al256(long x) { return (x + 255) & ~255L; }
 
-HnPlan hn_plan(long bq, long nd, int k, int rows) {
+HnPlan hn_plan(long bq, long nd, int k, int rows, long tpsm = SC_TPS_MAX) {
   HnPlan p{};
   p.nch = (nd + SC_COLS - 1) / SC_COLS;
   p.RT = (bq + rows - 1) / rows;
   long S = (256 + p.RT - 1) / p.RT;
-  const long smin = (p.nch + SC_TPS_MAX - 1) / SC_TPS_MAX;
+  const long smin = (p.nch + tpsm - 1) / tpsm;
   if (S < smin) S = smin;
   if (S > p.nch) S = p.nch;
   p.tps = (p.nch + S - 1) / S;
@@ -542,10 +605,24 @@ HnPlan hn_plan(long bq, long nd, int k, int rows) {
   return p;
 }
 
+template <int KS, int V>
+void hn_scan_launch(const bf16_t* qn, long bq, const bf16_t* dn, long nd, long label_offset, const HnPlan& p, float* CM,
+                    hipStream_t st) {
+  int map = tt::opt(tt::OPT_HN_MAP);
+  if (map == 2 && (p.RT % 2 != 0 || p.S % 4 != 0)) map = 0;
+  hipLaunchKernelGGL((hn_scan_kernel<KS, V>), dim3((unsigned)(p.RT * p.S)), dim3(ScanCfg<KS, V>::WAVES * 64), 0, st, qn,
+                     bq, dn, nd, label_offset, (int)p.S, (int)p.tps, p.nch, CM, map);
+}
+
 template <int KS>
 int hn_run(const bf16_t* qn, long bq, const bf16_t* dn, long nd, long label_offset, int k, int32_t* idx, float* val,
            char* ws, hipStream_t st) {
-  const HnPlan p = hn_plan(bq, nd, k, ScanCfg<KS>::ROWS);
+  int v = KS == 8 ? tt::opt(tt::OPT_HN_SCAN_V) : 0;
+  if (v != 4 && v != 5) v = 0;
+  if (v == 5 && bq * ((nd + SC_COLS - 1) / SC_COLS) * 4 >= (1L << 31)) v = 0;  // CM offsets in 32 bits
+  const HnPlan p = v == 4   ? hn_plan(bq, nd, k, ScanCfg<KS, 4>::ROWS, ScanCfg<KS, 4>::PLAN_TPS)
+                   : v == 5 ? hn_plan(bq, nd, k, ScanCfg<KS, 5>::ROWS, ScanCfg<KS, 5>::PLAN_TPS)
+                            : hn_plan(bq, nd, k, ScanCfg<KS>::ROWS);
   float* CM = reinterpret_cast<float*>(ws);
   int32_t* sel = reinterpret_cast<int32_t*>(ws + p.off_sel);
   float* cand = reinterpret_cast<float*>(ws + p.off_cand);
@@ -556,10 +633,16 @@ int hn_run(const bf16_t* qn, long bq, const bf16_t* dn, long nd, long label_offs
     // still reproduces every ranked value bit for bit
     TT_PROPAGATE(tt::tt_hn_scan_gemm(qn, bq, dn, nd, 32 * KS, label_offset, CM, p.nch, st));
   } else {
-    int map = tt::opt(tt::OPT_HN_MAP);
-    if (map == 2 && (p.RT % 2 != 0 || p.S % 4 != 0)) map = 0;
-    hipLaunchKernelGGL((hn_scan_kernel<KS>), dim3((unsigned)(p.RT * p.S)), dim3(ScanCfg<KS>::WAVES * 64), 0, st, qn, bq, dn, nd, label_offset, (int)p.S,
-                       (int)p.tps, p.nch, CM, map);
+    if constexpr (KS == 8) {
+      if (v == 4)
+        hn_scan_launch<KS, 4>(qn, bq, dn, nd, label_offset, p, CM, st);
+      else if (v == 5)
+        hn_scan_launch<KS, 5>(qn, bq, dn, nd, label_offset, p, CM, st);
+      else
+        hn_scan_launch<KS, 0>(qn, bq, dn, nd, label_offset, p, CM, st);
+    } else {
+      hn_scan_launch<KS, 0>(qn, bq, dn, nd, label_offset, p, CM, st);
+    }
     TT_CHECK_LAUNCH("hn_scan_kernel");
   }
   const dim3 rows4((unsigned)tt_ceil_div(bq, 4));

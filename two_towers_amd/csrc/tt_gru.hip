@@ -385,6 +385,21 @@ TT_DEV void unpack8(uint4 v, float (&f)[8]) {
 #ifndef TT_BWD_CREG  // gru_bwd_rows: the BPTT carry in registers (0: bf16 ping-pong buffer in HBM)
 #define TT_BWD_CREG 1
 #endif
+#ifndef TT_BWD_OUT_NT  // gru_bwd_rows: the dG_r / dG_z / dGh_n output stores non-temporal (1) or plain (0)
+#define TT_BWD_OUT_NT 0
+#endif
+// 8 floats -> 8 bf16 in one 16-byte store, non-temporal when NT
+template <bool NT>
+TT_DEV void st8_pol(bf16_t* p, const float (&f)[8]) {
+  if constexpr (NT) {
+    tt_u32x4 w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+    __builtin_nontemporal_store(w, reinterpret_cast<tt_u32x4*>(p));
+  } else {
+    st8(p, f);
+  }
+}
 
 // ---- backward step on 256x256 tiles (bf16): the recurrent GEMM on the 8-phase loop --
 // One workgroup (8 waves) per 256 rows x 256 hidden units of a recurrence: at B 8192,
@@ -949,10 +964,10 @@ __global__ __launch_bounds__(512) void gru_bwd_rows(BwdArgs a) {
       if constexpr (!CREG) st8(cr_cur + (long)bl * H + u0 + jg, cout);
       const long row = (long)b * T_ + t;
       bf16_t* xw = DGXw + row * a.ldd + u0 + jg;
-      st8(xw, o_r);
-      st8(xw + H, o_z);
+      st8_pol<TT_BWD_OUT_NT != 0>(xw, o_r);
+      st8_pol<TT_BWD_OUT_NT != 0>(xw + H, o_z);
       st8_sc1(grs, (int)(((long)bl * T_ * a.ldd + u0 + jg + 2 * H) * 2L), o_n, (bf16_t*)nullptr);
-      st8(DGHw + row * a.ldd + u0 + jg, o_hn);
+      st8_pol<TT_BWD_OUT_NT != 0>(DGHw + row * a.ldd + u0 + jg, o_hn);
     };
     auto batch = [&](const int kb) {
       uint4 vin[NB][7];

@@ -153,7 +153,7 @@ def cpu_baseline(args):
 # runs two chains of step kernels), hence the dispatches-per-step scaling.
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # the PMC summary of the build this tree ships (tools/pmc_bench.sh), named explicitly
-PMC_SUMMARY = os.path.join(_HERE, "profiles", "r05_pmc_summary.json")
+PMC_SUMMARY = os.path.join(_HERE, "profiles", "r06_pmc_summary.json")
 # the CPU baseline at the metric's own batch (bench.py --cpu-only --cpu-batch 8192 --cpu-steps 2)
 CPU_B8192 = os.path.join(_HERE, "profiles", "r04_cpu_baseline_b8192.json")
 REGION_KERNEL = {"gru_bwd": ("gru_bwd_step<", "gru_bwd_big", "gru_bwd_rows<"), "gru_fwd": ("gru_fwd_xs<", "gru_fwd_xcp<", "gru_fwd_seq<"),

@@ -472,7 +472,8 @@ TT_DEV void epi_quad_simple(const GemmArgs& g, const f32x4 (&acc)[8][4], bf16_t*
     const auto s1 = __builtin_amdgcn_permlane16_swap(w[0][1], w[1][1], false, false);
     const uint4 v = make_uint4(s0[0], s1[0], s0[1], s1[1]);
     const int off = (int)(((long)(wm + 16 * i + lr) * g.ldc + cs) * 2L);
-    if (g.stream_out) st16_sc1(crs, off, v);
+    if (g.stream_out == 2) st16_buf_aux<2>(crs, off, v);
+    else if (g.stream_out) st16_sc1(crs, off, v);
     else st16_buf(crs, (uint32_t)off, 0, v);
   }
 }
@@ -1202,7 +1203,7 @@ int launch_persist(int akout, int bkout, bool shift, const GemmArgs& g0, int nti
   if constexpr (std::is_same<TO, bf16_t>::value) {
     if (PERSIST_IEPI && tt::opt(tt::OPT_GEMM_IEPI) && !akout && !bkout && !shift && a3 && buf && g.M % 256 == 0 &&
         g.N % 256 == 0 && g.vec_ok && g.bias_vec_ok && g.alpha == 1.f && !g.relu && !g.drop_thresh && !g.beta &&
-        g.stream_out <= 1 && g.force_regstage == 0) {
+        g.stream_out <= 2 && g.force_regstage == 0) {
       hipLaunchKernelGGL((gemm_persist<T, false, false, false, TO, true, true, false, true>), grid, blk, 0, st, g, ntiles);
       TT_CHECK_LAUNCH("gemm_persist");
       return 0;

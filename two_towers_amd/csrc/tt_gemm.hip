@@ -615,6 +615,7 @@ __global__ __launch_bounds__(RB == 2 ? 512 : 256, 1) void gemm_bres(GemmArgs g, 
     return ld16_buf(ra, off, 0);
   };
   if (BRES_STAG > 0 && wave >= NW / 2) __builtin_amdgcn_s_sleep(BRES_STAG);
+  if (TT_PRIO_HALF && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   uint4 ar[PD][RB];
   int t = wave;
 #pragma unroll
@@ -818,6 +819,7 @@ __global__ __launch_bounds__(512) void gemm_persist(GemmArgs g, int ntiles) {
   }
   __builtin_amdgcn_s_barrier();
   const bool late = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;  // wave row 1
+  if (TT_PRIO_HALF && late) __builtin_amdgcn_s_setprio(1);
   if (late) __builtin_amdgcn_s_barrier();
 
   int git = 0;  // running K-tile index of the stream (slot parity)

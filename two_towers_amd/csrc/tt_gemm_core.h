@@ -26,6 +26,9 @@ typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
+#ifndef TT_PRIO_HALF  // 1: waves 4-7 of the 8-wave loops run at s_setprio 1 (the second-dispatched half)
+#define TT_PRIO_HALF 0
+#endif
 #ifndef TT_SHIFT_BUF  // 0: the time-shifted operand keeps per-piece pointer DMAs (the round-4 form)
 #define TT_SHIFT_BUF 1
 #endif
@@ -819,6 +822,7 @@ struct Loop8 {
     pb1.fix(0, base + 3 * HALF);
     __builtin_amdgcn_s_barrier();
     const bool late = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;  // wave row 1
+    if (TT_PRIO_HALF && late) __builtin_amdgcn_s_setprio(1);
     if (late) __builtin_amdgcn_s_barrier();
     uint4 fa[2][4], fb[2][4];
     for (int r = 0; r < kt1 - kt0; ++r) {
@@ -912,6 +916,7 @@ struct Loop8 {
     pb1.fix(0, base + BOFF + HALF);
     __builtin_amdgcn_s_barrier();
     const bool late = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;  // wave row 1
+    if (TT_PRIO_HALF && late) __builtin_amdgcn_s_setprio(1);
     if (late) __builtin_amdgcn_s_barrier();
     uint4 fa[2][4], fb[2][4];
     int as = 0;  // A slot of K-tile r (r mod 3)

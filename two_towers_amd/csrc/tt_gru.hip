@@ -1812,6 +1812,9 @@ __global__ __launch_bounds__(xc::NT, 1) __attribute__((amdgpu_waves_per_eu(1, 1)
 // so each SIMD's matrix pipe and vector issue are fed by different waves (MI355X_MICROARCH.md
 // "Two waves per SIMD"), with ONE barrier per chunk. The MFMA sequence per chunk and the
 // cell are gru_fwd_xcp's (same k order from zero, gru_cell): bit-identical outputs.
+#ifndef XS_VPRIO  // gru_fwd_xs: 1 = the vector waves run at s_setprio 1 (static priority experiment)
+#define XS_VPRIO 0
+#endif
 #ifndef XS_MPUB  // gru_fwd_xs: arrivals published by matrix wave 0 (0: by vector thread 0)
 #define XS_MPUB 1
 #endif
@@ -2011,6 +2014,7 @@ __global__ __launch_bounds__(xs::NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2)
 #pragma unroll
   for (int p = 0; p < QPW; ++p) hv[p] = tt_u32x4{0u, 0u, 0u, 0u};  // step 0, chunk 2
   __syncthreads();  // the matrix waves' chunk 0
+  if (XS_VPRIO) __builtin_amdgcn_s_setprio(1);  // the vector waves win VALU/issue arbitration
   for (int idx = 0; idx < NS; ++idx) {
     const bool has_next = idx + 1 < NS;
     const Step nxt = step_of(has_next ? idx + 1 : idx);

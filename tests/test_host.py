@@ -90,6 +90,25 @@ def test_library_exports_every_header_symbol():
     assert lib.tt_version().decode().startswith("tt_hip")
 
 
+def test_variant_switch_defaults_and_roundtrip():
+    """The kernel-variant switches (tt_set_option / tt_get_option, host-only) default to the
+    measured-fastest forms the bench and DESIGN.md quote, set and read back, and an unknown
+    name is an error, not a silent no-op."""
+    from two_towers_amd import _lib
+    expect = {"gru_fwd_xc": 1, "gru_fwd_xs": 1, "gru_xc_coop": 0, "gemm_persist": 1, "gemm_bres": 1,
+              "gemm_iepi": 1, "bres_rows": 32, "hn_scan_v": 5, "hn_map": 2, "hn_scan_gemm": 0, "hn_gemm": 0,
+              "gemm_stream_out": 1, "gru_bwd_persist": 1}
+    got = {k: _lib.get_option(k) for k in expect}
+    assert got == expect, got
+    old = _lib.set_option("hn_scan_v", 0)
+    try:
+        assert old == 5 and _lib.get_option("hn_scan_v") == 0
+    finally:
+        _lib.set_option("hn_scan_v", old)
+    with pytest.raises(RuntimeError):
+        _lib.set_option("no_such_switch", 1)
+
+
 def test_library_links_no_vendor_math_library():
     """Every kernel on the path is hand-written (north star: no dual backends): the shared
     library's dynamic dependencies name no vendor BLAS / DNN / GEMM library."""

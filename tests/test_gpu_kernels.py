@@ -262,6 +262,37 @@ def test_gemm_b_resident_matches_persistent(m, n, k, nb, with_bias, rows):
     assert rel_err(outs[0][0][rows].float(), ref) < 8e-3
 
 
+@pytest.mark.parametrize("m,n,k,nb,with_bias", [(70144, 3072, 1024, 2, True), (4096, 512, 64, 1, False),
+                                                (16384, 1536, 640, 2, True)])
+@pytest.mark.parametrize("form", [1, 2])
+def test_gemm_four_wave_kernel_matches_persistent(m, n, k, nb, with_bias, form):
+    """The four-wave 128x128-per-wave NT kernel (option gemm_w4: 1 LDS-DMA operand staging,
+    2 register staging) against the persistent
+    256x256 kernel on the same operands: same MFMA instruction, operand order (transposed
+    accumulate) and k order, so every bf16 output is identical. The layer-1 input-projection
+    class (K 1024, bias), a single 64-deep K-tile pair and a K that is not a power of two."""
+    from two_towers_amd._lib import option
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(m + n + k)
+    A = [torch.randn(m, k, generator=g, device=DEV).to(dt) for _ in range(nb)]
+    B = [(torch.randn(n, k, generator=g, device=DEV) * k ** -0.5).to(dt) for _ in range(nb)]
+    bias = [torch.randn(n, generator=g, device=DEV) for _ in range(nb)] if with_bias else None
+    outs = []
+    for w4 in (form, 0):
+        C = [torch.full((m, n), float("nan"), device=DEV, dtype=dt) for _ in range(nb)]
+        with option("gemm_w4", w4), option("gemm_bres", 0):
+            ops.gemm(A, B, C, m=m, n=n, k=k, lda=k, ldb=k, ldc=n, a_kouter=False, b_kouter=False, dtype=dt,
+                     out_dtype=dt, bias=bias, splits=1)
+        torch.cuda.synchronize()
+        outs.append(C)
+    for i in range(nb):
+        bad = int((outs[0][i].view(torch.int16) != outs[1][i].view(torch.int16)).sum())
+        assert bad == 0, f"batch {i}: {bad} of {m * n} outputs differ"
+    rows = torch.randint(0, m, (256,), generator=g, device=DEV)
+    ref = A[0][rows].float() @ B[0].float().t() + (bias[0] if with_bias else 0)
+    assert rel_err(outs[0][0][rows].float(), ref) < 8e-3
+
+
 def test_gemm_input_projection_l1_class_hand_written():
     """The layer-1 input-projection class (bf16, both operands K-contiguous, K 1024,
     M >= 65536, bias, bf16 out; enhanced_two_tower.py:51,57 via nn.GRU layer 1) runs on the

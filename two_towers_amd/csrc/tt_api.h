@@ -47,6 +47,7 @@ enum Opt {
   OPT_GEMM_IEPI,        // 1: the persistent GEMM's plain bf16 bias epilogue interleaved into the next tile's first K-tile
   OPT_BRES_ROWS,        // gemm_bres rows per wave tile: 32 (8 waves) or 64 (4 waves, each B fragment read feeds 4 MFMAs)
   OPT_HN_SCAN_V,        // h 256 hard-negative scan variant: 0 round-3 form, 4 64 queries per wave, 5 five-slot ring
+  OPT_GEMM_W4,          // 1: bf16 NT GEMMs with bias on the four-wave 128x128-per-wave kernel (gemm_w4)
   OPT_N
 };
 int opt(Opt o);

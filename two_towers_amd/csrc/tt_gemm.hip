@@ -43,7 +43,7 @@ constexpr OptDef kOpts[OPT_N] = {
     {"gemm_order", "TT_GEMM_ORDER", 0},           {"gru_step_ring", "TT_GRU_STEP_RING", 4},
     {"gru_fwd_xs", "TT_GRU_FWD_XS", 1},           {"hn_scan_gemm", "TT_HN_SCAN_GEMM", 0},
     {"gemm_iepi", "TT_GEMM_IEPI", 1},             {"bres_rows", "TT_BRES_ROWS", 32},
-    {"hn_scan_v", "TT_HN_SCAN_V", 5},
+    {"hn_scan_v", "TT_HN_SCAN_V", 5},             {"gemm_w4", "TT_GEMM_W4", 0},
 };
 struct OptTable {
   std::atomic<int> v[OPT_N];
@@ -1223,6 +1223,206 @@ int launch_persist(int akout, int bkout, bool shift, const GemmArgs& g0, int nti
   return 0;
 }
 
+// ---- four-wave 256x256 NT GEMM (option gemm_w4; bf16 in / out, bias) ------------------
+// The 8-wave loops above give each wave a 128x64 tile: per 32-deep K-slice the workgroup
+// reads 96 KiB of fragments from LDS for 4.2 MFLOP, which with the DMA writes fills the
+// LDS port for as long as the MFMAs run. Here 4 waves (one per SIMD, up to 512 registers)
+// own 128x128 tiles (256 accumulator registers, in AGPRs): 64 KiB of fragment reads per
+// K-slice, every fragment feeding 8 MFMAs. The K loop runs 32-deep K-tiles through a 4-slot
+// LDS ring (A and B images of 256 rows x 64 B, 16-byte chunk c of row r at slot
+// c ^ ((r >> 1) & 3)), three K-tiles of buffer LDS-DMAs in flight, one barrier per K-tile,
+// and the fragments of K-tile kt+1 read from LDS between the MFMAs of kt (double-buffered in
+// registers) so the one wave per SIMD always has MFMAs to issue. Same MFMA, operand order
+// (transposed accumulate) and k order as gemm_persist: bit-identical to it.
+namespace w4 {
+constexpr int SLOT = 32768;  // A image 16 KiB + B image 16 KiB
+constexpr int NS = 4;
+struct Frags {
+  uint4 a[8], b[8];
+};
+TT_DEV uint4 frag(const char* img, int r0) {
+  const int lane = threadIdx.x & 63;
+  const int row = r0 + (lane & 15);
+  return *reinterpret_cast<const uint4*>(img + row * 64 + (((lane >> 4) ^ ((row >> 1) & 3)) << 4));
+}
+}  // namespace w4
+
+// RS (option gemm_w4 2): the operand K-tiles are staged through registers instead of
+// LDS-DMA (one wave per SIMD pays each DMA piece's issue cost in its own MFMA stream):
+// 16-byte buffer loads of K-tile kt+3 issued during K-tile kt, written to LDS with
+// ds_write_b128 one step later, three LDS slots.
+template <bool RS>
+__global__ __launch_bounds__(256, 1) void gemm_w4(GemmArgs g, int ntm, int ntn) {
+  constexpr int NSL = RS ? 3 : w4::NS;
+  __shared__ __attribute__((aligned(16))) char lds[NSL * w4::SLOT];
+  const int id = ttg::xcd_remap(blockIdx.x, gridDim.x);
+  const int per = ntm * ntn;
+  const int bi = id / per, tile = id - bi * per;
+  const int mt = tile / ntn, nt = tile - mt * ntn;
+  const int m0 = mt * 256, n0 = nt * 256;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wr = wave >> 1, wc = wave & 1;
+  const bf16_t* A = static_cast<const bf16_t*>(g.a[bi]);
+  const bf16_t* B = static_cast<const bf16_t*>(g.b[bi]);
+  const uint32_t base = __builtin_amdgcn_readfirstlane(ttg::lds_addr_of(lds));
+  // this wave's 8 DMA pieces per K-tile: pieces 8 wave .. 8 wave + 7 of 32 (0-15 A rows
+  // 16p.., 16-31 B rows 16(p-16)..); lane -> (row, chunk slot) of the 1 KiB piece
+  const bool isA = wave < 2;
+  const long ld = isA ? g.lda : g.ldb;
+  const long r0 = isA ? m0 : n0;
+  const long rows_left = (isA ? g.M : g.N) - r0;
+  const long nrec = rows_left * ld * 2;
+  const uint32_t nrec32 = (uint32_t)(nrec > 0xFFFFFFFFL ? 0xFFFFFFFFL : nrec);
+  const ttg::tt_rsrc4 rs = ttg::make_rsrc4((isA ? A : B) + r0 * ld, nrec32);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>((isA ? A : B) + r0 * ld), (short)0, (int)(nrec32 > 0x7fffffffu ? 0x7fffffffu : nrec32), 0x00020000);
+  // piece j of this wave covers operand rows 16 ((wave & 1) 8 + j) + (lane >> 2); the chunk
+  // swizzle (row >> 1) & 3 = (lane >> 3) & 3 does not depend on j, so one per-lane offset
+  // serves every piece and the piece's row advance rides in the SGPR soffset with the K-tile's
+  const int prow = 16 * (wave & 1) * 8 + (lane >> 2);
+  const uint32_t voff = (uint32_t)(prow * ld * 2 + (((lane & 3) ^ ((lane >> 3) & 3)) << 4));
+  const uint32_t pstep = (uint32_t)(16 * ld * 2);
+  const uint32_t pbase = (uint32_t)wave * 8u * 1024u;  // this wave's first piece in a slot
+  auto dma = [&](int kt, int j) {
+    ttg::dma16_buf(rs, voff, (uint32_t)kt * 64u + (uint32_t)j * pstep,
+                   base + (uint32_t)(kt % NSL) * w4::SLOT + pbase + (uint32_t)j * 1024u);
+  };
+  auto gload = [&](int kt, int j) { return ld16_buf(rsb, voff, (int)((uint32_t)kt * 64u + (uint32_t)j * pstep)); };
+  auto lput = [&](int kt, int j, const uint4& v) {
+    *reinterpret_cast<uint4*>(lds + (kt % NSL) * w4::SLOT + pbase + j * 1024 + lane * 16) = v;
+  };
+  const int nk = g.K / 32;
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (RS) {
+    // K-tiles 0, 1 through registers into slots 0, 1; K-tile 2's loads in flight in S1
+    uint4 S0[8], S1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) S0[j] = gload(0, j);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) S1[j] = gload(1, j);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lput(0, j, S0[j]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lput(1, j, S1[j]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) S0[j] = gload(2, j);
+    __syncthreads();
+    w4::Frags F0, F1;
+    {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        F0.a[i] = w4::frag(lds, wr * 128 + 16 * i);
+        F0.b[i] = w4::frag(lds + 16384, wc * 128 + 16 * i);
+      }
+    }
+    // step kt: slot (kt+1) % 3 holds K-tile kt+1 (written during step kt-1); Sw holds K-tile
+    // kt+2's global data (loaded during step kt-1), written now into slot (kt+2) % 3 -- last
+    // read during step kt-2 (K-tile kt-1), so free after step kt-1's barrier; K-tile kt+3's
+    // loads go into Sw as its values are written
+    auto step = [&](const w4::Frags& Fc, w4::Frags& Fn, uint4 (&Sw)[8], int kt) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's writes of K-tile kt+1
+      __builtin_amdgcn_s_barrier();
+      const char* img = lds + ((kt + 1) % NSL) * w4::SLOT;
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        Fn.a[i] = w4::frag(img, wr * 128 + 16 * i);
+        Fn.b[i] = w4::frag(img + 16384, wc * 128 + 16 * i);
+        lput(kt + 2, i, Sw[i]);
+        Sw[i] = gload(kt + 3, i);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = ttg::mma<bf16_t>(Fc.b[j], Fc.a[i], acc[i][j]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+      step(F0, F1, S0, kt);
+      step(F1, F0, S0, kt + 1);
+    }
+    (void)S1;
+  } else {
+    // Every K-tile step issues the same work whether or not it is needed (K-tiles past the
+    // end are read from the next rows / zeros into slots nothing reads, and the last step's
+    // next-fragment reads are discarded), so the loop has no branches and the waits are
+    // constant: younger than K-tile kt+1's pieces are only K-tile kt+2's, 8 per wave.
+    // prologue: K-tiles 0..2 in flight, wait for 0
+#pragma unroll
+    for (int kt = 0; kt < 3; ++kt)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dma(kt, j);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    w4::Frags F0, F1;
+    {
+      const char* img = lds;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        F0.a[i] = w4::frag(img, wr * 128 + 16 * i);
+        F0.b[i] = w4::frag(img + 16384, wc * 128 + 16 * i);
+      }
+    }
+    // one K-tile: its MFMAs from Fc, K-tile kt+1's fragments into Fn between them, and K-tile
+    // kt+3's DMA pieces, one per row block
+    auto step = [&](const w4::Frags& Fc, w4::Frags& Fn, int kt) {
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // K-tile kt+1 landed (this wave's pieces)
+      __builtin_amdgcn_s_barrier();  // ... everyone's; and every wave is done with slot (kt+3) % 4
+      const char* img = lds + ((kt + 1) % w4::NS) * w4::SLOT;
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        Fn.a[i] = w4::frag(img, wr * 128 + 16 * i);
+        Fn.b[i] = w4::frag(img + 16384, wc * 128 + 16 * i);
+        dma(kt + 3, i);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = ttg::mma<bf16_t>(Fc.b[j], Fc.a[i], acc[i][j]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    // nk even here (the host requires K % 64 == 0)
+    for (int kt = 0; kt < nk; kt += 2) {
+      step(F0, F1, kt);
+      step(F1, F0, kt + 1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing DMAs land before the LDS is released
+  }
+  // epilogue: acc[i][j][e] = C(row wr*128 + 16 i + (lane & 15), col wc*128 + 16 j + 4 (lane >> 4) + e)
+  bf16_t* C = static_cast<bf16_t*>(g.c[bi]);
+  const float* bias = g.bias[bi];
+  const int q = lane >> 4, lr = lane & 15;
+  const __amdgpu_buffer_rsrc_t crs = tt_rsrc(C + (long)m0 * g.ldc + n0);
+#pragma unroll
+  for (int jp = 0; jp < 4; ++jp) {
+    float bv[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 b4 = bias ? *reinterpret_cast<const float4*>(bias + n0 + wc * 128 + 16 * (2 * jp + h) + 4 * q)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+      bv[h][0] = b4.x; bv[h][1] = b4.y; bv[h][2] = b4.z; bv[h][3] = b4.w;
+    }
+    const int cs = wc * 128 + 16 * (2 * jp + (q & 1)) + 8 * (q >> 1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      uint32_t w[2][2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 a = acc[i][2 * jp + h];
+        w[h][0] = (uint32_t)f2bf(a[0] + bv[h][0]) | ((uint32_t)f2bf(a[1] + bv[h][1]) << 16);
+        w[h][1] = (uint32_t)f2bf(a[2] + bv[h][2]) | ((uint32_t)f2bf(a[3] + bv[h][3]) << 16);
+      }
+      const auto s0 = __builtin_amdgcn_permlane16_swap(w[0][0], w[1][0], false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(w[0][1], w[1][1], false, false);
+      const uint4 v = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      const int off = (int)(((long)(wr * 128 + 16 * i + lr) * g.ldc + cs) * 2L);
+      if (g.stream_out) st16_sc1(crs, off, v);
+      else st16_buf(crs, (uint32_t)off, 0, v);
+    }
+  }
+}
+
 // gemm_bres where it applies (bf16 NT, bias only, N % 192 == 0, short K): returns true if launched
 template <typename T, typename TO>
 bool try_bres(int akout, int bkout, bool shift, const GemmArgs& g, int nbatch, hipStream_t st, int* rc) {
@@ -1295,6 +1495,21 @@ int launch_gemm(int akout, int bkout, bool shift, GemmArgs& g, int nbatch, hipSt
       if (!g.a[b]) continue;
       const long d = (long)((const char*)g.a_hi[b] - (const char*)g.a[b]) / (long)sizeof(T);
       if (d < 0 || d + (g.M - g.a_split) > g.lda) buf = false;
+    }
+  }
+  if constexpr (std::is_same<T, bf16_t>::value && std::is_same<TO, bf16_t>::value) {
+    // gemm_w4 (opt-in): NT, whole 256x256 tiles, K a multiple of 64, bias only
+    if (tt::opt(tt::OPT_GEMM_W4) && !akout && !bkout && !shift && g.splits == 1 && !g.beta && !g.relu &&
+        !g.drop_thresh && g.alpha == 1.f && g.force_regstage == 0 && g.M % 256 == 0 && g.N % 256 == 0 && g.K % 64 == 0 &&
+        g.K >= 32 && g.vec_ok && g.bias_vec_ok && (g.lda * 2) % 16 == 0 && (g.ldb * 2) % 16 == 0 &&
+        256L * g.lda * 2 < (1L << 31) && 256L * g.ldb * 2 < (1L << 31) && 256L * g.ldc * 2 < (1L << 31)) {
+      const int ntm = g.M / 256, ntn = g.N / 256;
+      if (tt::opt(tt::OPT_GEMM_W4) == 2)
+        hipLaunchKernelGGL(gemm_w4<true>, dim3((unsigned)(ntm * ntn * nbatch)), dim3(256), 0, st, g, ntm, ntn);
+      else
+        hipLaunchKernelGGL(gemm_w4<false>, dim3((unsigned)(ntm * ntn * nbatch)), dim3(256), 0, st, g, ntm, ntn);
+      TT_CHECK_LAUNCH("gemm_w4");
+      return 0;
     }
   }
   if (dma && persist_ok && !shift && (g.force_regstage == 0 || g.force_regstage >= 9) && g.splits == 1 && !g.beta && nk >= 2 && nk <= tt::opt(tt::OPT_GEMM_PERSIST_MAXK) && t256 >= 512 &&

@@ -1234,6 +1234,9 @@ int launch_persist(int akout, int bkout, bool shift, const GemmArgs& g0, int nti
 // and the fragments of K-tile kt+1 read from LDS between the MFMAs of kt (double-buffered in
 // registers) so the one wave per SIMD always has MFMAs to issue. Same MFMA, operand order
 // (transposed accumulate) and k order as gemm_persist: bit-identical to it.
+#ifndef W4_LEAD  // gemm_w4 (LDS-DMA form): K-tiles in flight beyond the next (2; 3 = slot kt % 4 refilled
+#define W4_LEAD 2    // with K-tile kt+4 as soon as every wave holds kt's fragments; measured no faster)
+#endif
 namespace w4 {
 constexpr int SLOT = 32768;  // A image 16 KiB + B image 16 KiB
 constexpr int NS = 4;
@@ -1349,12 +1352,12 @@ __global__ __launch_bounds__(256, 1) void gemm_w4(GemmArgs g, int ntm, int ntn) 
     // end are read from the next rows / zeros into slots nothing reads, and the last step's
     // next-fragment reads are discarded), so the loop has no branches and the waits are
     // constant: younger than K-tile kt+1's pieces are only K-tile kt+2's, 8 per wave.
-    // prologue: K-tiles 0..2 in flight, wait for 0
+    // prologue: K-tiles 0..W4_LEAD in flight, wait for 0
 #pragma unroll
-    for (int kt = 0; kt < 3; ++kt)
+    for (int kt = 0; kt <= W4_LEAD; ++kt)
 #pragma unroll
       for (int j = 0; j < 8; ++j) dma(kt, j);
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 * W4_LEAD) : "memory");
     __builtin_amdgcn_s_barrier();
     w4::Frags F0, F1;
     {
@@ -1368,15 +1371,19 @@ __global__ __launch_bounds__(256, 1) void gemm_w4(GemmArgs g, int ntm, int ntn) 
     // one K-tile: its MFMAs from Fc, K-tile kt+1's fragments into Fn between them, and K-tile
     // kt+3's DMA pieces, one per row block
     auto step = [&](const w4::Frags& Fc, w4::Frags& Fn, int kt) {
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // K-tile kt+1 landed (this wave's pieces)
-      __builtin_amdgcn_s_barrier();  // ... everyone's; and every wave is done with slot (kt+3) % 4
+      // K-tile kt+1 landed (this wave's pieces; younger: K-tiles kt+2 .. kt+W4_LEAD)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 * (W4_LEAD - 1)) : "memory");
+      // W4_LEAD 3 refills slot kt % 4, whose fragments (K-tile kt, read during step kt-1) must
+      // have reached every wave's registers before the barrier
+      if (W4_LEAD >= 3) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // ... everyone's; and every wave is done with slot (kt+W4_LEAD+1) % 4
       const char* img = lds + ((kt + 1) % w4::NS) * w4::SLOT;
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         Fn.a[i] = w4::frag(img, wr * 128 + 16 * i);
         Fn.b[i] = w4::frag(img + 16384, wc * 128 + 16 * i);
-        dma(kt + 3, i);
+        dma(kt + W4_LEAD + 1, i);
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[i][j] = ttg::mma<bf16_t>(Fc.b[j], Fc.a[i], acc[i][j]);
         __builtin_amdgcn_sched_barrier(0);
